@@ -1,0 +1,355 @@
+"""MI355X GPT-2 decode engine: hand-written HIP kernels + hipGraph-captured decode steps.
+
+One engine instance owns one tensor-parallel group's share of the model (TP=1 on a single
+MI355X, or one rank of a TP group; one process per GPU, RCCL over xGMI for the collectives).
+
+Semantics are the reference's ``model.generate(max_length=150, repetition_penalty=1.2)``
+greedy decode (``tutoring_server.py:21-29``): full sequences are returned (prompt echoed),
+each ends at EOS (inclusive) or at ``max_length`` total tokens.
+
+Per decode step (SURVEY.md §7.1 design choice 3), replayed as ONE hipGraph per batch bucket:
+
+    for each layer:  LN1 -> QKV GEMM (+bias, q out, k/v scattered into the KV cache)
+                     -> row attention over the cache -> out-proj GEMM (+bias +residual)
+                     [-> RCCL all-reduce of the partial residual under TP]
+                     -> LN2 -> c_fc GEMM (+bias, GELU-tanh) -> c_proj GEMM (+bias +residual)
+                     [-> all-reduce]
+    ln_f -> LM-head GEMM with repetition penalty + argmax fused in the epilogue
+         [-> all-gather of the (value, index) keys across vocab shards]
+    -> device-side update: token append, seen bitmap, stop flags, next embedding.
+
+No host round trip happens inside a step; the host only checks the stop flags every few steps.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.config import GPT2Config
+from .weights import GPT2DeviceWeights, prepare_gpt2_weights
+
+
+@dataclass
+class GenerateStats:
+    batch: int = 0
+    prompt_tokens: int = 0
+    new_tokens: int = 0
+    prefill_ms: float = 0.0
+    decode_ms: float = 0.0
+    steps: int = 0
+    graph: bool = False
+
+    @property
+    def total_ms(self) -> float:
+        return self.prefill_ms + self.decode_ms
+
+
+def seen_bitmap(tokens, words: int) -> np.ndarray:
+    """Repetition-penalty bitmap of a token list, as int32 words (bit t%32 of word t//32)."""
+    bm = np.zeros(words, dtype=np.uint32)
+    ids = np.asarray(sorted(set(int(t) for t in tokens)), dtype=np.int64)
+    if ids.size:
+        np.bitwise_or.at(bm, ids >> 5, (np.uint32(1) << (ids & 31).astype(np.uint32)))
+    return bm.view(np.int32)
+
+
+def _bucket(n: int) -> int:
+    for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024):
+        if n <= b:
+            return b
+    return (n + 255) // 256 * 256
+
+
+class HipGPT2Engine:
+    def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
+                 max_batch: int = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
+                 check_every: int = 16):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
+        ops.lib()  # fail loudly if the kernel library is missing
+        self.cfg = cfg
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.tp_group = tp_group
+        if tp_group is not None:
+            import torch.distributed as dist
+
+            self.tp_rank, self.tp_size = dist.get_rank(tp_group), dist.get_world_size(tp_group)
+        else:
+            self.tp_rank, self.tp_size = 0, 1
+        if isinstance(weights, GPT2DeviceWeights):
+            self.w = weights
+        else:
+            self.w = prepare_gpt2_weights(cfg, weights, self.device, self.tp_rank, self.tp_size)
+        self.max_batch = max_batch
+        self.max_length = max_length
+        if max_length > cfg.n_positions:
+            raise ValueError("max_length exceeds n_positions")
+        self.use_graph = use_graph
+        self.check_every = check_every
+        self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._alloc_state()
+
+    # ------------------------------------------------------------------ state
+    def _alloc_state(self):
+        cfg, B, dev = self.cfg, self.max_batch, self.device
+        D, Dl, Fl, Hl = cfg.n_embd, self.w.d_local, self.w.ffn_local, self.w.n_heads_local
+        T = self.max_length
+        i32, f32, bf = torch.int32, torch.float32, torch.bfloat16
+        # KV cache [L][2][slots][H_local][T][64]: sized for the batch at full length.
+        self.kv = torch.zeros(cfg.n_layer, 2, B, Hl, T, 64, dtype=bf, device=dev)
+        self.x = torch.zeros(B, D, dtype=f32, device=dev)
+        self.y = torch.zeros(B, D, dtype=f32, device=dev)
+        self.h = torch.zeros(B, D, dtype=bf, device=dev)
+        self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
+        self.att = torch.zeros(B, Dl, dtype=bf, device=dev)
+        self.ff = torch.zeros(B, Fl, dtype=bf, device=dev)
+        self.local_keys = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.all_keys = torch.zeros(self.tp_size, B, dtype=torch.int64, device=dev)
+        self.lens = torch.zeros(B, dtype=i32, device=dev)
+        self.finished = torch.ones(B, dtype=i32, device=dev)
+        self.out_tokens = torch.zeros(B, T, dtype=i32, device=dev)
+        self.seen_words = cfg.vocab_padded // 32
+        self.seen = torch.zeros(B, self.seen_words, dtype=i32, device=dev)
+        self.cur_tok = torch.zeros(B, dtype=i32, device=dev)
+        self.cur_pos = torch.zeros(B, dtype=i32, device=dev)
+        self.cur_kvlen = torch.ones(B, dtype=i32, device=dev)
+        self.slots = torch.arange(B, dtype=i32, device=dev)
+
+    def kv_cache_bytes(self) -> int:
+        return self.kv.numel() * self.kv.element_size()
+
+    # ------------------------------------------------------------------ collectives
+    def _all_reduce(self, t: torch.Tensor):
+        if self.tp_size > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(t, group=self.tp_group)
+
+    def _gather_keys(self, B: int) -> torch.Tensor:
+        """Keys of every vocab shard as [tp, B] (all-gather of 8 B per row per rank)."""
+        if self.tp_size > 1:
+            import torch.distributed as dist
+
+            flat = self.all_keys.view(-1)[: self.tp_size * B]
+            dist.all_gather_into_tensor(flat, self.local_keys[:B], group=self.tp_group)
+            return flat.view(self.tp_size, B)
+        return self.local_keys[:B]
+
+    # ------------------------------------------------------------------ transformer body
+    def _layers(self, x: torch.Tensor, y: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int):
+        """Run all blocks on rows [0, M) of the residual ``x`` (in place; ``y`` is TP scratch)."""
+        w, cfg = self.w, self.cfg
+        eps = cfg.layer_norm_epsilon
+        tp = self.tp_size > 1
+        xs, hs, qs, ats, ffs = x[:M], h[:M], q[:M], att[:M], ff[:M]
+        ys = y[:M]
+        for li, lw in enumerate(w.layers):
+            kc, vc = self.kv[li, 0], self.kv[li, 1]
+            ops.layernorm(xs, lw.ln1_g, lw.ln1_b, eps, out_bf16=hs)
+            ops.gemm(hs, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
+                     row_slot=row_slot, row_pos=row_pos)
+            ops.row_attention(qs, kc, vc, row_slot, row_kvlen, out=ats)
+            if tp:
+                ops.gemm(ats, lw.w_o, ops.EPI_F32, bias=lw.b_o, out=ys, resid=xs if self.tp_rank == 0 else None)
+                self._all_reduce(ys)
+                res = ys
+            else:
+                ops.gemm(ats, lw.w_o, ops.EPI_F32, bias=lw.b_o, out=xs, resid=xs)
+                res = xs
+            ops.layernorm(res, lw.ln2_g, lw.ln2_b, eps, out_bf16=hs)
+            ops.gemm(hs, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs)
+            if tp:
+                ops.gemm(ffs, lw.w_p, ops.EPI_F32, bias=lw.b_p, out=xs, resid=ys if self.tp_rank == 0 else None)
+                self._all_reduce(xs)
+            else:
+                ops.gemm(ffs, lw.w_p, ops.EPI_F32, bias=lw.b_p, out=xs, resid=xs)
+
+    def _lm_head_and_update(self, hidden_bf16: torch.Tensor, B: int, penalty: float):
+        cfg = self.cfg
+        ops.gemm(hidden_bf16, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.local_keys[:B], seen=self.seen[:B],
+                 vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
+        keys = self._gather_keys(B)
+        ops.decode_update(keys, self.local_keys[:B], self.lens[:B], self.finished[:B], self.out_tokens[:B],
+                          self.seen[:B], self.cur_tok[:B], self.cur_pos[:B], self.cur_kvlen[:B], self.w.wte,
+                          self.w.wpe, self.x[:B], cfg.eos_token_id, self.max_length)
+
+    def _decode_step(self, B: int, penalty: float):
+        self._layers(self.x, self.y, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
+                     self.cur_kvlen[:B], B)
+        ops.layernorm(self.x[:B], self.w.lnf_g, self.w.lnf_b, self.cfg.layer_norm_epsilon, out_bf16=self.h[:B])
+        self._lm_head_and_update(self.h[:B], B, penalty)
+
+    def _graph_for(self, B: int, penalty: float) -> torch.cuda.CUDAGraph:
+        key = (B, float(penalty))
+        g = self._graphs.get(key)
+        if g is None:
+            # warm up on a side stream (kernel code objects loaded, RCCL comm initialised)
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            saved = self._snapshot_state(B)
+            with torch.cuda.stream(s):
+                self._decode_step(B, penalty)
+            torch.cuda.current_stream().wait_stream(s)
+            self._restore_state(B, saved)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._decode_step(B, penalty)
+            self._restore_state(B, saved)
+            self._graphs[key] = g
+        return g
+
+    def _snapshot_state(self, B: int):
+        return [t[:B].clone() for t in (self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok,
+                                        self.cur_pos, self.cur_kvlen, self.x, self.local_keys)]
+
+    def _restore_state(self, B: int, saved):
+        for t, s in zip((self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
+                         self.cur_kvlen, self.x, self.local_keys), saved):
+            t[:B].copy_(s)
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill(self, prompts: list[list[int]], B: int, penalty: float):
+        cfg, dev = self.cfg, self.device
+        n = len(prompts)
+        lens = [len(p) for p in prompts]
+        R = sum(lens)
+        tokens = torch.tensor([t for p in prompts for t in p], dtype=torch.int32)
+        pos = torch.tensor([i for L in lens for i in range(L)], dtype=torch.int32)
+        slot = torch.tensor([b for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32)
+        last = torch.tensor([sum(lens[: b + 1]) - 1 for b in range(n)] + [R - 1] * (B - n), dtype=torch.int32)
+        tokens_d, pos_d, slot_d = (t.to(dev, non_blocking=True) for t in (tokens, pos, slot))
+        kvlen_d = pos_d + 1
+        last_d = last.to(dev, non_blocking=True)
+
+        # host-side sequence state for the batch bucket (rows >= n are inert: finished)
+        T = self.max_length
+        out_tok = torch.zeros(B, T, dtype=torch.int32)
+        seen = torch.zeros(B, self.seen_words, dtype=torch.int32)
+        lens_t = torch.ones(B, dtype=torch.int32)
+        fin = torch.ones(B, dtype=torch.int32)
+        for b, p in enumerate(prompts):
+            out_tok[b, : len(p)] = torch.tensor(p, dtype=torch.int32)
+            seen[b] = torch.from_numpy(seen_bitmap(p, self.seen_words))
+            lens_t[b] = len(p)
+            fin[b] = 1 if len(p) >= T else 0
+        for b in range(n, B):
+            out_tok[b, 0] = cfg.eos_token_id
+        self.out_tokens[:B].copy_(out_tok, non_blocking=True)
+        self.seen[:B].copy_(seen, non_blocking=True)
+        self.lens[:B].copy_(lens_t, non_blocking=True)
+        self.finished[:B].copy_(fin, non_blocking=True)
+        self.local_keys[:B].zero_()
+
+        D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
+        f32, bf = torch.float32, torch.bfloat16
+        x = ops.embed(tokens_d, pos_d, self.w.wte, self.w.wpe)
+        y = torch.empty(R, D, dtype=f32, device=dev) if self.tp_size > 1 else x
+        h = torch.empty(R, D, dtype=bf, device=dev)
+        q = torch.empty(R, Dl, dtype=bf, device=dev)
+        att = torch.empty(R, Dl, dtype=bf, device=dev)
+        ff = torch.empty(R, Fl, dtype=bf, device=dev)
+        self._layers(x, y, h, q, att, ff, slot_d, pos_d, kvlen_d, R)
+        hl = ops.layernorm_gather(x, last_d, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon)
+        self._lm_head_and_update(hl, B, penalty)
+
+    @torch.no_grad()
+    def prefill_last_hidden(self, prompts: list[list[int]]) -> torch.Tensor:
+        """ln_f(hidden) of each prompt's last token after a packed prefill (bf16 -> f32); test hook."""
+        cfg, dev = self.cfg, self.device
+        lens = [len(p) for p in prompts]
+        R = sum(lens)
+        tokens = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=dev)
+        pos = torch.tensor([i for L in lens for i in range(L)], dtype=torch.int32, device=dev)
+        slot = torch.tensor([b for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32, device=dev)
+        last = torch.tensor([sum(lens[: b + 1]) - 1 for b in range(len(prompts))], dtype=torch.int32, device=dev)
+        D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
+        x = ops.embed(tokens, pos, self.w.wte, self.w.wpe)
+        y = torch.empty(R, D, device=dev) if self.tp_size > 1 else x
+        bf = torch.bfloat16
+        h, q, att, ff = (torch.empty(R, n, dtype=bf, device=dev) for n in (D, Dl, Dl, Fl))
+        self._layers(x, y, h, q, att, ff, slot, pos, pos + 1, R)
+        return ops.layernorm_gather(x, last, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon).float()
+
+    # ------------------------------------------------------------------ public API
+    @torch.no_grad()
+    def generate(self, prompts: list[list[int]], max_length: int | None = None, repetition_penalty: float = 1.2,
+                 stats: GenerateStats | None = None) -> list[list[int]]:
+        T = self.max_length if max_length is None else max_length
+        if T != self.max_length:
+            raise ValueError(f"engine built for max_length={self.max_length}, got {T}")
+        n = len(prompts)
+        if n == 0:
+            return []
+        if n > self.max_batch:
+            out: list[list[int]] = []
+            for i in range(0, n, self.max_batch):
+                out += self.generate(prompts[i: i + self.max_batch], max_length, repetition_penalty, stats)
+            return out
+        prompts = [list(p)[-T:] if len(p) else [self.cfg.eos_token_id] for p in prompts]
+        B = min(_bucket(n), self.max_batch)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev2 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        self._prefill(prompts, B, repetition_penalty)
+        ev1.record()
+        steps_max = T - min(len(p) for p in prompts) - 1
+        graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
+        steps = 0
+        while steps < steps_max:
+            chunk = min(self.check_every, steps_max - steps)
+            for _ in range(chunk):
+                if graph is not None:
+                    graph.replay()
+                else:
+                    self._decode_step(B, repetition_penalty)
+            steps += chunk
+            if steps < steps_max and bool(self.finished[:n].all()):
+                break
+        ev2.record()
+        lens = self.lens[:n].cpu().tolist()
+        toks = self.out_tokens[:n].cpu()
+        res = [toks[b, : lens[b]].tolist() for b in range(n)]
+        if stats is not None:
+            ev2.synchronize()
+            stats.batch += n
+            stats.prompt_tokens += sum(len(p) for p in prompts)
+            stats.new_tokens += sum(lens[b] - len(prompts[b]) for b in range(n))
+            stats.prefill_ms += ev0.elapsed_time(ev1)
+            stats.decode_ms += ev1.elapsed_time(ev2)
+            stats.steps += steps
+            stats.graph = graph is not None
+        return res
+
+
+class TorchGPT2Engine:
+    """CPU (or any-device) engine on the plain-torch reference model: BASELINE config 1."""
+
+    def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor], device="cpu", max_length: int = 150,
+                 dtype=torch.float32):
+        from ..models.gpt2 import GPT2Reference
+
+        self.cfg = cfg
+        self.max_length = max_length
+        self.model = GPT2Reference(cfg, weights, device=device, dtype=dtype)
+
+    @torch.no_grad()
+    def generate(self, prompts: list[list[int]], max_length: int | None = None, repetition_penalty: float = 1.2,
+                 stats: GenerateStats | None = None) -> list[list[int]]:
+        from ..models.gpt2 import reference_generate
+
+        T = self.max_length if max_length is None else max_length
+        prompts = [list(p)[-T:] if len(p) else [self.cfg.eos_token_id] for p in prompts]
+        t0 = time.perf_counter()
+        out = reference_generate(self.model, prompts, max_length=T, repetition_penalty=repetition_penalty)
+        if stats is not None:
+            stats.batch += len(prompts)
+            stats.prompt_tokens += sum(map(len, prompts))
+            stats.new_tokens += sum(len(o) - len(p) for o, p in zip(out, prompts))
+            stats.decode_ms += (time.perf_counter() - t0) * 1e3
+        return out

@@ -1,0 +1,133 @@
+"""Convert HF-layout GPT-2 weights into the device layouts the HIP kernels consume, sharded for
+Megatron-style tensor parallelism.
+
+Kernel layout: every GEMM weight is stored [N][K] (K contiguous, "TN"), bf16; biases and LN
+parameters stay fp32.  TP sharding:
+
+* attention: column-parallel QKV by head (uneven head counts allowed, e.g. GPT-2-XL's 25 heads
+  over 8 ranks -> 4,3,3,3,3,3,3,3), row-parallel out-projection;
+* MLP: column-parallel c_fc, row-parallel c_proj (64-column granules);
+* LM head: vocab-parallel over the tied ``wte`` (shard boundaries on 64-row tiles) with a
+  fused local argmax and a cross-rank (value, index) max.
+
+Row-parallel biases live on rank 0 only, so the all-reduce of the partial sums yields exactly
+``x + bias + sum(partials)``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from ..models.config import GPT2Config
+
+
+def split_even(n: int, parts: int) -> list[int]:
+    base, rem = divmod(n, parts)
+    return [base + (1 if i < rem else 0) for i in range(parts)]
+
+
+def shard_range(n: int, parts: int, rank: int) -> tuple[int, int]:
+    sizes = split_even(n, parts)
+    start = sum(sizes[:rank])
+    return start, start + sizes[rank]
+
+
+@dataclass
+class LayerWeights:
+    ln1_g: torch.Tensor
+    ln1_b: torch.Tensor
+    w_qkv: torch.Tensor  # [3*Dl, D]
+    b_qkv: torch.Tensor  # [3*Dl]
+    w_o: torch.Tensor  # [D, Dl]
+    b_o: torch.Tensor | None  # [D] on rank 0
+    ln2_g: torch.Tensor
+    ln2_b: torch.Tensor
+    w_fc: torch.Tensor  # [Fl, D]
+    b_fc: torch.Tensor  # [Fl]
+    w_p: torch.Tensor  # [D, Fl]
+    b_p: torch.Tensor | None  # [D] on rank 0
+
+
+@dataclass
+class GPT2DeviceWeights:
+    cfg: GPT2Config
+    tp_rank: int
+    tp_size: int
+    head_range: tuple[int, int]
+    ffn_range: tuple[int, int]
+    vocab_range: tuple[int, int]  # padded-vocab rows of the LM head shard
+    wte: torch.Tensor  # [Vpad, D] bf16 (full; embedding gather + LM head view)
+    wpe: torch.Tensor  # [P, D] bf16
+    lnf_g: torch.Tensor
+    lnf_b: torch.Tensor
+    layers: list[LayerWeights] = field(default_factory=list)
+
+    @property
+    def n_heads_local(self) -> int:
+        return self.head_range[1] - self.head_range[0]
+
+    @property
+    def d_local(self) -> int:
+        return 64 * self.n_heads_local
+
+    @property
+    def ffn_local(self) -> int:
+        return self.ffn_range[1] - self.ffn_range[0]
+
+    @property
+    def lm_head(self) -> torch.Tensor:
+        return self.wte[self.vocab_range[0]: self.vocab_range[1]]
+
+    def nbytes(self) -> int:
+        n = self.wte.numel() * 2 + self.wpe.numel() * 2
+        for lw in self.layers:
+            for t in (lw.w_qkv, lw.w_o, lw.w_fc, lw.w_p):
+                n += t.numel() * t.element_size()
+        return n
+
+
+def prepare_gpt2_weights(cfg: GPT2Config, w: dict[str, torch.Tensor], device, tp_rank: int = 0, tp_size: int = 1,
+                         dtype=torch.bfloat16) -> GPT2DeviceWeights:
+    D, H, hd = cfg.n_embd, cfg.n_head, cfg.head_dim
+    assert hd == 64, "kernels assume 64-wide heads (all GPT-2 sizes)"
+    h0, h1 = shard_range(H, tp_size, tp_rank)
+    if h1 <= h0:
+        raise ValueError(f"tp_size={tp_size} leaves rank {tp_rank} with no attention heads (H={H})")
+    ft = cfg.n_inner // 64
+    f0, f1 = (x * 64 for x in shard_range(ft, tp_size, tp_rank))
+    vt = cfg.vocab_padded // 64
+    v0, v1 = (x * 64 for x in shard_range(vt, tp_size, tp_rank))
+
+    def dev(t, dt=dtype):
+        return t.to(device=device, dtype=dt).contiguous()
+
+    f32 = torch.float32
+    wte = torch.zeros(cfg.vocab_padded, D, dtype=f32)
+    wte[: cfg.vocab_size] = w["transformer.wte.weight"].float()
+    out = GPT2DeviceWeights(
+        cfg=cfg, tp_rank=tp_rank, tp_size=tp_size, head_range=(h0, h1), ffn_range=(f0, f1), vocab_range=(v0, v1),
+        wte=dev(wte), wpe=dev(w["transformer.wpe.weight"]),
+        lnf_g=dev(w["transformer.ln_f.weight"], f32), lnf_b=dev(w["transformer.ln_f.bias"], f32),
+    )
+    cols = slice(h0 * hd, h1 * hd)
+    for i in range(cfg.n_layer):
+        p = f"transformer.h.{i}."
+        wa = w[p + "attn.c_attn.weight"].float()  # [D, 3D]
+        ba = w[p + "attn.c_attn.bias"].float()
+        q, k, v = wa[:, :D], wa[:, D: 2 * D], wa[:, 2 * D:]
+        bq, bk, bv = ba[:D], ba[D: 2 * D], ba[2 * D:]
+        w_qkv = torch.cat([q[:, cols], k[:, cols], v[:, cols]], dim=1).t()
+        b_qkv = torch.cat([bq[cols], bk[cols], bv[cols]])
+        wo = w[p + "attn.c_proj.weight"].float()[cols, :].t()  # [D, Dl]
+        wfc = w[p + "mlp.c_fc.weight"].float()[:, f0:f1].t()  # [Fl, D]
+        wp = w[p + "mlp.c_proj.weight"].float()[f0:f1, :].t()  # [D, Fl]
+        out.layers.append(LayerWeights(
+            ln1_g=dev(w[p + "ln_1.weight"], f32), ln1_b=dev(w[p + "ln_1.bias"], f32),
+            w_qkv=dev(w_qkv), b_qkv=dev(b_qkv, f32),
+            w_o=dev(wo), b_o=dev(w[p + "attn.c_proj.bias"], f32) if tp_rank == 0 else None,
+            ln2_g=dev(w[p + "ln_2.weight"], f32), ln2_b=dev(w[p + "ln_2.bias"], f32),
+            w_fc=dev(wfc), b_fc=dev(w[p + "mlp.c_fc.bias"].float()[f0:f1], f32),
+            w_p=dev(wp), b_p=dev(w[p + "mlp.c_proj.bias"], f32) if tp_rank == 0 else None,
+        ))
+    return out

@@ -1,0 +1,353 @@
+"""Python binding for the hand-written CDNA4 (gfx950) HIP kernel library.
+
+The kernels live in ``ops/csrc/*.hip`` and are compiled with ``hipcc --offload-arch=gfx950``
+into ONE in-tree shared library, ``ops/_lib/libdlms_hip.so`` (plain C ABI, no torch headers,
+seconds to build).  It is loaded with ``ctypes`` AFTER ``torch`` so that it binds to the HIP
+runtime torch already loaded (same SONAME ``libamdhip64.so.7``), hence shares streams, the
+caching allocator's memory and hipGraph capture with torch.
+
+Every wrapper checks shapes/dtypes/devices on the host before launching (a bad launch on the
+box can reset the GPU), launches on ``torch.cuda.current_stream()`` and raises on any HIP
+error.  There is deliberately NO silent PyTorch fallback: if the library is missing on a GPU
+host, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from pathlib import Path
+
+import torch
+
+_HERE = Path(__file__).resolve().parent
+CSRC = _HERE / "csrc"
+LIB_DIR = _HERE / "_lib"
+LIB_PATH = LIB_DIR / "libdlms_hip.so"
+SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip"]
+ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
+
+EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX = range(6)
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _sources() -> list[Path]:
+    return [CSRC / s for s in SOURCES]
+
+
+def needs_build() -> bool:
+    if not LIB_PATH.exists():
+        return True
+    t = LIB_PATH.stat().st_mtime
+    deps = _sources() + list(CSRC.glob("*.h"))
+    return any(p.stat().st_mtime > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every kernel source for gfx950 into the in-tree shared library."""
+    if not force and not needs_build():
+        return LIB_PATH
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH.with_suffix(f".so.tmp{os.getpid()}")
+    cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
+           "-Wno-unused-result", "-o", str(tmp)] + [str(s) for s in _sources()]
+    if verbose:
+        print(" ".join(cmd))
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+class GemmEpi(ctypes.Structure):
+    _fields_ = [
+        ("bias", ctypes.c_void_p), ("out", ctypes.c_void_p), ("ldo", ctypes.c_int),
+        ("resid", ctypes.c_void_p), ("ldr", ctypes.c_int),
+        ("q_out", ctypes.c_void_p), ("ldq", ctypes.c_int),
+        ("k_cache", ctypes.c_void_p), ("v_cache", ctypes.c_void_p),
+        ("row_slot", ctypes.c_void_p), ("row_pos", ctypes.c_void_p),
+        ("n_heads", ctypes.c_int), ("t_max", ctypes.c_int), ("d_local", ctypes.c_int),
+        ("argmax_out", ctypes.c_void_p), ("seen", ctypes.c_void_p),
+        ("seen_words", ctypes.c_int), ("vocab", ctypes.c_int), ("col_offset", ctypes.c_int),
+        ("penalty", ctypes.c_float),
+    ]
+
+
+def _bind(L):
+    P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    sig = {
+        "dlms_gemm": [I, P, I, P, I, I, I, I, ctypes.POINTER(GemmEpi), P],
+        "dlms_layernorm": [P, I, P, P, P, I, P, I, I, I, F, P],
+        "dlms_layernorm_gather": [P, I, P, P, P, P, I, I, I, F, P],
+        "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
+        "dlms_embed": [P, P, P, P, P, I, I, I, P],
+        "dlms_decode_update": [P, I, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I, I, P],
+        "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
+        "dlms_mean_pool": [P, P, P, P, I, I, P],
+        "dlms_cosine": [P, P, P, I, I, I, F, P],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    L.dlms_error_string.argtypes = [ctypes.c_int]
+    L.dlms_error_string.restype = ctypes.c_char_p
+    L.dlms_gemm_epi_size.restype = ctypes.c_int
+    if L.dlms_gemm_epi_size() != ctypes.sizeof(GemmEpi):
+        raise RuntimeError("GemmEpi ABI mismatch between ctypes mirror and compiled library")
+
+
+def lib():
+    """Load (building first if needed) the kernel library.  Raises if it cannot be loaded."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if needs_build():
+                build()
+            L = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+            _bind(L)
+            _lib = L
+    return _lib
+
+
+def available() -> bool:
+    """True when a GPU is present (the HIP library will then be required, not optional)."""
+    return torch.cuda.is_available()
+
+
+def _check(err: int, what: str):
+    if err != 0:
+        raise RuntimeError(f"{what} failed: HIP error {err} ({lib().dlms_error_string(err).decode()})")
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _req(t: torch.Tensor, dtype, name: str, dim: int | None = None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be on the GPU")
+    if dim is not None and t.dim() != dim:
+        raise ValueError(f"{name}: expected {dim}-D, got {tuple(t.shape)}")
+    if t.dim() >= 1 and t.stride(-1) != 1:
+        raise ValueError(f"{name}: last dim must be contiguous")
+
+
+# ---------------------------------------------------------------------------------------------
+# GEMM
+# ---------------------------------------------------------------------------------------------
+def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, out=None, resid=None,
+         q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
+         argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0):
+    """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0)."""
+    _req(a, torch.bfloat16, "a", 2)
+    _req(w, torch.bfloat16, "w", 2)
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2 or K % 64 or N % 64:
+        raise ValueError(f"gemm shapes a{tuple(a.shape)} w{tuple(w.shape)}: need matching K%64==0, N%64==0")
+    ep = GemmEpi()
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() < N:
+            raise ValueError("bias too short")
+        ep.bias = bias.data_ptr()
+    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32):
+        want = torch.float32 if epi == EPI_F32 else torch.bfloat16
+        if out is None:
+            out = torch.empty(M, N, dtype=want, device=a.device)
+        _req(out, want, "out", 2)
+        if out.shape[0] < M or out.shape[1] < N:
+            raise ValueError("out too small")
+        ep.out, ep.ldo = out.data_ptr(), out.stride(0)
+        if resid is not None:
+            _req(resid, torch.float32, "resid", 2)
+            if resid.shape[0] < M or resid.shape[1] < N:
+                raise ValueError("resid too small")
+            ep.resid, ep.ldr = resid.data_ptr(), resid.stride(0)
+    elif epi == EPI_QKV:
+        for t, n in ((q_out, "q_out"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+            _req(t, torch.bfloat16, n)
+        _req(row_slot, torch.int32, "row_slot", 1)
+        _req(row_pos, torch.int32, "row_pos", 1)
+        if N % 3:
+            raise ValueError("QKV N must be 3*d_local")
+        d_local = N // 3
+        if d_local % 64:
+            raise ValueError("d_local must be a multiple of the 64-wide head")
+        if k_cache.dim() != 4 or k_cache.shape != v_cache.shape or k_cache.shape[1] * 64 != d_local or k_cache.shape[3] != 64:
+            raise ValueError(f"cache shape {tuple(k_cache.shape)} incompatible with d_local={d_local}")
+        if q_out.shape[0] < M or q_out.shape[1] < d_local or row_slot.numel() < M or row_pos.numel() < M:
+            raise ValueError("qkv epilogue buffers too small")
+        ep.q_out, ep.ldq = q_out.data_ptr(), q_out.stride(0)
+        ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
+        ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
+        ep.n_heads, ep.t_max, ep.d_local = k_cache.shape[1], k_cache.shape[2], d_local
+        out = q_out
+    elif epi == EPI_ARGMAX:
+        _req(argmax_out, torch.int64, "argmax_out", 1)
+        _req(seen, torch.int32, "seen", 2)
+        if argmax_out.numel() < M or seen.shape[0] < M or seen.shape[1] * 32 < vocab:
+            raise ValueError("argmax epilogue buffers too small")
+        ep.argmax_out, ep.seen = argmax_out.data_ptr(), seen.data_ptr()
+        ep.seen_words, ep.vocab, ep.col_offset, ep.penalty = seen.stride(0), vocab, col_offset, penalty
+        out = argmax_out
+    else:
+        raise ValueError(f"unknown epilogue {epi}")
+    _check(lib().dlms_gemm(epi, _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, ctypes.byref(ep), _stream()),
+           "dlms_gemm")
+    return out
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, *, out_bf16=None,
+              out_f32=None, want_bf16: bool = True):
+    _req(x, torch.float32, "x", 2)
+    M, D = x.shape
+    _req(gamma, torch.float32, "gamma", 1)
+    _req(beta, torch.float32, "beta", 1)
+    if gamma.numel() != D or beta.numel() != D or D % 4 or D > 2048:
+        raise ValueError("layernorm: bad gamma/beta/D")
+    if want_bf16 and out_bf16 is None:
+        out_bf16 = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+    if out_bf16 is not None:
+        _req(out_bf16, torch.bfloat16, "out_bf16", 2)
+        if out_bf16.shape[0] < M or out_bf16.shape[1] < D:
+            raise ValueError("out_bf16 too small")
+    if out_f32 is not None:
+        _req(out_f32, torch.float32, "out_f32", 2)
+        if out_f32.shape[0] < M or out_f32.shape[1] < D:
+            raise ValueError("out_f32 too small")
+    _check(lib().dlms_layernorm(_p(x), x.stride(0), _p(gamma), _p(beta), _p(out_bf16),
+                                out_bf16.stride(0) if out_bf16 is not None else 0, _p(out_f32),
+                                out_f32.stride(0) if out_f32 is not None else 0, M, D, float(eps), _stream()),
+           "dlms_layernorm")
+    return out_bf16 if out_bf16 is not None else out_f32
+
+
+def layernorm_gather(x: torch.Tensor, rows: torch.Tensor, gamma, beta, eps: float, out_bf16=None):
+    _req(x, torch.float32, "x", 2)
+    _req(rows, torch.int32, "rows", 1)
+    M, D = rows.numel(), x.shape[1]
+    if out_bf16 is None:
+        out_bf16 = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+    _req(out_bf16, torch.bfloat16, "out_bf16", 2)
+    if D % 4 or D > 2048 or gamma.numel() != D:
+        raise ValueError("layernorm_gather: bad D")
+    _check(lib().dlms_layernorm_gather(_p(x), x.stride(0), _p(rows), _p(gamma), _p(beta), _p(out_bf16),
+                                       out_bf16.stride(0), M, D, float(eps), _stream()), "dlms_layernorm_gather")
+    return out_bf16
+
+
+def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
+                  row_kvlen: torch.Tensor, out: torch.Tensor | None = None, scale: float | None = None):
+    """q: bf16 [R, H*64]; caches bf16 [slots, H, t_max, 64]; row r attends keys [0, row_kvlen[r])."""
+    _req(q, torch.bfloat16, "q", 2)
+    _req(k_cache, torch.bfloat16, "k_cache", 4)
+    _req(v_cache, torch.bfloat16, "v_cache", 4)
+    _req(row_slot, torch.int32, "row_slot", 1)
+    _req(row_kvlen, torch.int32, "row_kvlen", 1)
+    R = q.shape[0]
+    S, H, T, hd = k_cache.shape
+    if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64 or T > 2048:
+        raise ValueError("row_attention: bad shapes")
+    if row_slot.numel() < R or row_kvlen.numel() < R:
+        raise ValueError("row_attention: index arrays too short")
+    if out is None:
+        out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=q.device)
+    _req(out, torch.bfloat16, "out", 2)
+    sc = (1.0 / 8.0) if scale is None else scale
+    _check(lib().dlms_row_attention(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
+                                    _p(out), out.stride(0), R, H, T, float(sc), _stream()), "dlms_row_attention")
+    return out
+
+
+def embed(tokens: torch.Tensor, positions: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, out=None):
+    _req(tokens, torch.int32, "tokens", 1)
+    _req(positions, torch.int32, "positions", 1)
+    _req(wte, torch.bfloat16, "wte", 2)
+    _req(wpe, torch.bfloat16, "wpe", 2)
+    R, D = tokens.numel(), wte.shape[1]
+    if out is None:
+        out = torch.empty(R, D, dtype=torch.float32, device=tokens.device)
+    _req(out, torch.float32, "out", 2)
+    _check(lib().dlms_embed(_p(tokens), _p(positions), _p(wte), _p(wpe), _p(out), out.stride(0), R, D, _stream()),
+           "dlms_embed")
+    return out
+
+
+def decode_update(keys: torch.Tensor, local_keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok, cur_pos,
+                  cur_kvlen, wte, wpe, x, eos: int, t_max: int):
+    _req(keys, torch.int64, "keys")
+    _req(local_keys, torch.int64, "local_keys", 1)
+    B = local_keys.numel()
+    world = keys.numel() // B
+    for t, n in ((lens, "lens"), (finished, "finished"), (cur_tok, "cur_tok"), (cur_pos, "cur_pos"),
+                 (cur_kvlen, "cur_kvlen")):
+        _req(t, torch.int32, n, 1)
+        if t.numel() < B:
+            raise ValueError(f"{n} too short")
+    _req(out_tokens, torch.int32, "out_tokens", 2)
+    _req(seen, torch.int32, "seen", 2)
+    _req(x, torch.float32, "x", 2)
+    D = wte.shape[1]
+    if out_tokens.shape[0] < B or x.shape[0] < B or x.shape[1] < D:
+        raise ValueError("decode_update: buffers too small")
+    _check(lib().dlms_decode_update(_p(keys), world, _p(local_keys), _p(lens), _p(finished), _p(out_tokens),
+                                    out_tokens.stride(0), _p(seen), seen.stride(0), _p(cur_tok), _p(cur_pos),
+                                    _p(cur_kvlen), _p(wte), _p(wpe), _p(x), x.stride(0), B, D, eos, t_max, _stream()),
+           "dlms_decode_update")
+
+
+def bert_embed_ln(ids, positions, word, pos_emb, type0, gamma, beta, eps: float, out_f32=None, out_bf16=None):
+    _req(ids, torch.int32, "ids", 1)
+    _req(positions, torch.int32, "positions", 1)
+    for t, n in ((word, "word"), (pos_emb, "pos_emb")):
+        _req(t, torch.float32, n, 2)
+    R, D = ids.numel(), word.shape[1]
+    if out_f32 is None:
+        out_f32 = torch.empty(R, D, dtype=torch.float32, device=ids.device)
+    if out_bf16 is None:
+        out_bf16 = torch.empty(R, D, dtype=torch.bfloat16, device=ids.device)
+    _check(lib().dlms_bert_embed_ln(_p(ids), _p(positions), _p(word), _p(pos_emb), _p(type0), _p(gamma), _p(beta),
+                                    _p(out_f32), _p(out_bf16), R, D, float(eps), _stream()), "dlms_bert_embed_ln")
+    return out_f32, out_bf16
+
+
+def mean_pool(x: torch.Tensor, start: torch.Tensor, length: torch.Tensor, out=None):
+    _req(x, torch.float32, "x", 2)
+    _req(start, torch.int32, "start", 1)
+    _req(length, torch.int32, "length", 1)
+    S, D = start.numel(), x.shape[1]
+    if not x.is_contiguous():
+        raise ValueError("mean_pool: x must be contiguous")
+    if out is None:
+        out = torch.empty(S, D, dtype=torch.float32, device=x.device)
+    _check(lib().dlms_mean_pool(_p(x), _p(start), _p(length), _p(out), S, D, _stream()), "dlms_mean_pool")
+    return out
+
+
+def cosine(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-8, out=None):
+    _req(a, torch.float32, "a", 2)
+    _req(b, torch.float32, "b", 2)
+    if a.shape[1] != b.shape[1] or not a.is_contiguous() or not b.is_contiguous():
+        raise ValueError("cosine: bad shapes")
+    if out is None:
+        out = torch.empty(a.shape[0], b.shape[0], dtype=torch.float32, device=a.device)
+    _check(lib().dlms_cosine(_p(a), _p(b), _p(out), a.shape[0], b.shape[0], a.shape[1], float(eps), _stream()),
+           "dlms_cosine")
+    return out

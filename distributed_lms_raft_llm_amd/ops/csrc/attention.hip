@@ -1,0 +1,115 @@
+// Row attention over a slot-addressed KV cache (K5 decode, K6/K14 fallback path).
+//
+// Cache layout: [slots][H][t_max][64] bf16 for K and for V (one contiguous 128-B row per key, so a
+// wave-instruction of 8 keys x 8 lanes x 16 B reads 1 KiB contiguous).
+// Query row r attends keys [0, row_kvlen[r]) of slot row_slot[r]: causal GPT-2 decode/prefill passes
+// kvlen = pos + 1, the bidirectional BERT encoder passes kvlen = sequence length.
+// Scores for the whole row live in LDS (t_max <= 2048), so the softmax is an exact two-pass one.
+#include "common.h"
+
+#define ATT_MAX_T 2048
+
+__global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                            const bf16_t* __restrict__ kc,
+                                                            const bf16_t* __restrict__ vc,
+                                                            const int* __restrict__ row_slot,
+                                                            const int* __restrict__ row_kvlen, bf16_t* out,
+                                                            int ldo, int H, int t_max, float scale) {
+    __shared__ float sc[ATT_MAX_T];
+    __shared__ float red[4][64];
+    __shared__ float stat[2];
+
+    const int h = blockIdx.x;
+    const int r = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int kk = lane >> 3;  // key within the wave's group of 8
+    const int c = lane & 7;    // 8-dim chunk of the head
+    const int slot = row_slot[r];
+    int kvlen = row_kvlen[r];
+    kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
+
+    const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+    const bf16_t* K = kc + head_off;
+    const bf16_t* V = vc + head_off;
+
+    float qf[8];
+    unpack8(*reinterpret_cast<const uint4*>(q + (size_t)r * ldq + h * 64 + c * 8), qf);
+
+    // ---- scores ----
+    for (int t0 = wave * 8; t0 < kvlen; t0 += 32) {
+        const int t = t0 + kk;
+        float s = 0.f;
+        if (t < kvlen) {
+            float kf[8];
+            unpack8(*reinterpret_cast<const uint4*>(K + (size_t)t * 64 + c * 8), kf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
+        }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        if (c == 0 && t < kvlen) sc[t] = s * scale;
+    }
+    __syncthreads();
+
+    // ---- softmax statistics ----
+    float m = -INFINITY;
+    for (int t = tid; t < kvlen; t += 256) m = fmaxf(m, sc[t]);
+    m = wave_max(m);
+    if (lane == 0) red[wave][0] = m;
+    __syncthreads();
+    if (tid == 0) stat[0] = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+    __syncthreads();
+    m = stat[0];
+    float l = 0.f;
+    for (int t = tid; t < kvlen; t += 256) {
+        const float p = __expf(sc[t] - m);
+        sc[t] = p;
+        l += p;
+    }
+    l = wave_sum(l);
+    __syncthreads();
+    if (lane == 0) red[wave][1] = l;
+    __syncthreads();
+    if (tid == 0) stat[1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+    __syncthreads();
+
+    // ---- P . V ----
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t = wave * 8 + kk; t < kvlen; t += 32) {
+        float vf[8];
+        unpack8(*reinterpret_cast<const uint4*>(V + (size_t)t * 64 + c * 8), vf);
+        const float p = sc[t];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += p * vf[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        acc[j] += __shfl_xor(acc[j], 8, 64);
+        acc[j] += __shfl_xor(acc[j], 16, 64);
+        acc[j] += __shfl_xor(acc[j], 32, 64);
+    }
+    __syncthreads();  // red[] reuse
+    if (kk == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wave][c * 8 + j] = acc[j];
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const float inv = 1.f / stat[1];
+        const float o = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) * inv;
+        out[(size_t)r * ldo + h * 64 + tid] = f32_to_bf16(o);
+    }
+}
+
+extern "C" hipError_t dlms_row_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
+                                         const int* row_kvlen, void* out, int ldo, int R, int H, int t_max,
+                                         float scale, hipStream_t stream) {
+    if (t_max > ATT_MAX_T || R <= 0 || H <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(row_attention_kernel, dim3(H, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
+                       reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen,
+                       reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale);
+    return hipGetLastError();
+}

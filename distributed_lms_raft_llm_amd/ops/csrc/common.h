@@ -1,0 +1,127 @@
+// Shared device helpers for the CDNA4 (gfx950) kernel library.
+// Wave = 64 lanes everywhere; bf16 is carried as raw ushort and converted in-register.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DLMS_WAVE 64
+
+typedef unsigned short bf16_t;
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // one 16x16x32 MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // one 16x16x32 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+    return __uint_as_float(((unsigned int)v) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 (inputs are finite activations; NaN handling not needed
+// on this path, but keep NaN a NaN anyway by forcing the quiet bit).
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+    unsigned int u = __float_as_uint(f);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ unsigned int pack_bf16x2(float lo, float hi) {
+    return (unsigned int)f32_to_bf16(lo) | ((unsigned int)f32_to_bf16(hi) << 16);
+}
+
+// unpack 8 bf16 held in a uint4 into floats
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+    f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+    f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+    uint4 r;
+    r.x = pack_bf16x2(f[0], f[1]); r.y = pack_bf16x2(f[2], f[3]);
+    r.z = pack_bf16x2(f[4], f[5]); r.w = pack_bf16x2(f[6], f[7]);
+    return r;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+    const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+    const float k1 = 0.044715f;
+    float u = k0 * (x + k1 * x * x * x);
+    return 0.5f * x * (1.0f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+    return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f));
+}
+
+// Order-preserving map f32 -> u32 (larger float => larger unsigned).
+__device__ __forceinline__ unsigned int f32_ordered(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float f32_from_ordered(unsigned int o) {
+    unsigned int u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+    return __uint_as_float(u);
+}
+
+// argmax key: high 32 bits = ordered value (xor sign so the int64 compare is monotone),
+// low 32 bits = ~index so that ties resolve to the LOWEST index (torch.argmax semantics).
+__device__ __forceinline__ long long argmax_key(float v, int idx) {
+    unsigned long long hi = (unsigned long long)(f32_ordered(v) ^ 0x80000000u);
+    unsigned long long lo = (unsigned long long)(~(unsigned int)idx);
+    return (long long)((hi << 32) | lo);
+}
+
+__device__ __forceinline__ int argmax_key_index(long long k) {
+    return (int)(~(unsigned int)((unsigned long long)k & 0xffffffffull));
+}
+
+// XCD-aware bijective remap of a linear block id so that consecutive logical tiles land on one
+// XCD (8 XCDs, private L2 each; dispatch is round-robin over XCDs).  Speed only, never needed
+// for correctness (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg / 8, r = nwg % 8;
+    const int xcd = orig % 8;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + orig / 8;
+}
+
+// Epilogue parameters of the MFMA GEMM (gemm.hip).  Mirrored field-for-field by the ctypes
+// binding (ops/__init__.py); dlms_gemm_epi_size() lets Python assert the layouts agree.
+struct GemmEpi {
+    const float* bias;   // [N] or nullptr
+    void* out;           // bf16 or f32 output
+    int ldo;
+    const float* resid;  // f32 residual (EPI_F32) or nullptr
+    int ldr;
+    // EPI_QKV
+    bf16_t* q_out;
+    int ldq;
+    bf16_t* k_cache;
+    bf16_t* v_cache;
+    const int* row_slot;
+    const int* row_pos;
+    int n_heads;
+    int t_max;
+    int d_local;
+    // EPI_ARGMAX
+    unsigned long long* argmax_out;
+    const unsigned int* seen;
+    int seen_words;
+    int vocab;       // number of valid global vocab ids
+    int col_offset;  // global id of local column 0 (vocab-parallel shards)
+    float penalty;
+};

@@ -1,0 +1,104 @@
+// Token/position embedding (K1) and the per-step greedy bookkeeping that closes the decode loop
+// on the device (K11/K12 consumer), so a whole decode step replays as one hipGraph with no host
+// round trip: argmax key -> token -> output buffer, seen-bitmap, stop flags, next embedding.
+#include "common.h"
+
+// x[r] = wte[tokens[r]] + wpe[positions[r]]   (bf16 tables, f32 residual stream).  Wave per row.
+__global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ tokens, const int* __restrict__ positions,
+                                                    const bf16_t* __restrict__ wte, const bf16_t* __restrict__ wpe,
+                                                    float* x, int ldx, int R, int D) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const bf16_t* a = wte + (size_t)tokens[r] * D;
+    const bf16_t* b = wpe + (size_t)positions[r] * D;
+    float* o = x + (size_t)r * ldx;
+    for (int c = lane; c < D / 8; c += 64) {
+        float fa[8], fb[8];
+        unpack8(*reinterpret_cast<const uint4*>(a + c * 8), fa);
+        unpack8(*reinterpret_cast<const uint4*>(b + c * 8), fb);
+        float4 lo = make_float4(fa[0] + fb[0], fa[1] + fb[1], fa[2] + fb[2], fa[3] + fb[3]);
+        float4 hi = make_float4(fa[4] + fb[4], fa[5] + fb[5], fa[6] + fb[6], fa[7] + fb[7]);
+        reinterpret_cast<float4*>(o + c * 8)[0] = lo;
+        reinterpret_cast<float4*>(o + c * 8)[1] = hi;
+    }
+}
+
+// One wave per live sequence b.
+//   keys[w][b]   packed (ordered value, ~index) argmax keys from each of `world` vocab shards
+//   lens[b]      tokens so far (prompt + generated);  finished[b] stop flag
+//   out_tokens   [B][max_len] full sequences (prompt already written by the host)
+//   seen         [B][seen_words] repetition-penalty bitmap
+// Writes the next forward's token/position/kv-length for row b, its embedding into x, and clears
+// the local argmax slot for the next LM-head pass.
+__global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long long* __restrict__ keys, int world,
+                                                            unsigned long long* local_keys, int* lens, int* finished,
+                                                            int* out_tokens, int max_len, unsigned int* seen,
+                                                            int seen_words, int* cur_tok, int* cur_pos, int* cur_kvlen,
+                                                            const bf16_t* __restrict__ wte,
+                                                            const bf16_t* __restrict__ wpe, float* x, int ldx, int B,
+                                                            int D, int eos, int t_max) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B) return;
+    int tok = 0, pos = 0;
+    if (lane == 0) {
+        unsigned long long best = 0ull;
+        for (int w = 0; w < world; ++w) {
+            const unsigned long long k = keys[(size_t)w * B + b];
+            best = k > best ? k : best;
+        }
+        local_keys[b] = 0ull;
+        int len = lens[b];
+        if (!finished[b]) {
+            // best == 0 means no shard produced a candidate (cannot happen for vocab >= 1); stay in
+            // bounds anyway by emitting EOS.
+            tok = best ? (int)(~(unsigned int)(best & 0xffffffffull)) : eos;
+            out_tokens[(size_t)b * max_len + len] = tok;
+            seen[(size_t)b * seen_words + (tok >> 5)] |= 1u << (tok & 31);
+            len += 1;
+            lens[b] = len;
+            if (tok == eos || len >= max_len) finished[b] = 1;
+        } else {
+            tok = out_tokens[(size_t)b * max_len + (len - 1)];
+        }
+        pos = len - 1;
+        pos = pos < t_max - 1 ? pos : t_max - 1;
+        cur_tok[b] = tok;
+        cur_pos[b] = pos;
+        cur_kvlen[b] = pos + 1;
+    }
+    tok = __shfl(tok, 0, 64);
+    pos = __shfl(pos, 0, 64);
+    const bf16_t* a = wte + (size_t)tok * D;
+    const bf16_t* p = wpe + (size_t)pos * D;
+    float* o = x + (size_t)b * ldx;
+    for (int c = lane; c < D / 8; c += 64) {
+        float fa[8], fb[8];
+        unpack8(*reinterpret_cast<const uint4*>(a + c * 8), fa);
+        unpack8(*reinterpret_cast<const uint4*>(p + c * 8), fb);
+        reinterpret_cast<float4*>(o + c * 8)[0] = make_float4(fa[0] + fb[0], fa[1] + fb[1], fa[2] + fb[2], fa[3] + fb[3]);
+        reinterpret_cast<float4*>(o + c * 8)[1] = make_float4(fa[4] + fb[4], fa[5] + fb[5], fa[6] + fb[6], fa[7] + fb[7]);
+    }
+}
+
+extern "C" hipError_t dlms_embed(const int* tokens, const int* positions, const void* wte, const void* wpe, float* x,
+                                 int ldx, int R, int D, hipStream_t stream) {
+    if (D % 8 != 0 || R <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(embed_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, tokens, positions,
+                       reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, R, D);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int world, unsigned long long* local_keys,
+                                         int* lens, int* finished, int* out_tokens, int max_len, unsigned int* seen,
+                                         int seen_words, int* cur_tok, int* cur_pos, int* cur_kvlen, const void* wte,
+                                         const void* wpe, float* x, int ldx, int B, int D, int eos, int t_max,
+                                         hipStream_t stream) {
+    if (D % 8 != 0 || B <= 0 || world <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, world, local_keys, lens,
+                       finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
+                       reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, B, D, eos,
+                       t_max);
+    return hipGetLastError();
+}

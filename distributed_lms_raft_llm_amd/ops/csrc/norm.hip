@@ -1,0 +1,121 @@
+// LayerNorm family (K2, K13).  One wave per row, the whole row held in registers
+// (float4 loads, up to 8 per lane => d <= 2048), two-pass statistics in fp32.
+#include "common.h"
+
+#define LN_MAX_V4 8  // float4 per lane -> d <= 64*4*8 = 2048
+
+// y = LN(x) * gamma + beta.   x: f32 [M, ldx].  Writes bf16 (ldb) and/or f32 (ldf) outputs.
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int ldx,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, bf16_t* out_bf16, int ldb,
+                                                        float* out_f32, int ldf, int M, int D, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int nv = D >> 2;
+    const float4* xr = reinterpret_cast<const float4*>(x + (size_t)row * ldx);
+    float4 v[LN_MAX_V4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        v[i] = c < nv ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+            ss += (a * a + b * b) + (cc * cc + d * d);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+    const float4* g4 = reinterpret_cast<const float4*>(gamma);
+    const float4* b4 = reinterpret_cast<const float4*>(beta);
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            const float4 g = g4[c], b = b4[c];
+            float4 y;
+            y.x = (v[i].x - mean) * rstd * g.x + b.x;
+            y.y = (v[i].y - mean) * rstd * g.y + b.y;
+            y.z = (v[i].z - mean) * rstd * g.z + b.z;
+            y.w = (v[i].w - mean) * rstd * g.w + b.w;
+            if (out_f32) reinterpret_cast<float4*>(out_f32 + (size_t)row * ldf)[c] = y;
+            if (out_bf16) {
+                uint2 p;
+                p.x = pack_bf16x2(y.x, y.y);
+                p.y = pack_bf16x2(y.z, y.w);
+                reinterpret_cast<uint2*>(out_bf16 + (size_t)row * ldb)[c] = p;
+            }
+        }
+    }
+}
+
+// Gather variant: normalise only rows idx[0..M) of x (LM head on the last prompt token of each
+// sequence after a packed prefill).
+__global__ __launch_bounds__(256) void layernorm_gather_kernel(const float* __restrict__ x, int ldx,
+                                                               const int* __restrict__ rows,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, bf16_t* out_bf16,
+                                                               int ldb, int M, int D, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= M) return;
+    const int row = rows[r];
+    const int nv = D >> 2;
+    const float4* xr = reinterpret_cast<const float4*>(x + (size_t)row * ldx);
+    float4 v[LN_MAX_V4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        v[i] = c < nv ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+            ss += (a * a + b * b) + (cc * cc + d * d);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+    const float4* g4 = reinterpret_cast<const float4*>(gamma);
+    const float4* b4 = reinterpret_cast<const float4*>(beta);
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            const float4 g = g4[c], b = b4[c];
+            uint2 p;
+            p.x = pack_bf16x2((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y);
+            p.y = pack_bf16x2((v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+            reinterpret_cast<uint2*>(out_bf16 + (size_t)r * ldb)[c] = p;
+        }
+    }
+}
+
+extern "C" hipError_t dlms_layernorm(const float* x, int ldx, const float* gamma, const float* beta, void* out_bf16,
+                                     int ldb, float* out_f32, int ldf, int M, int D, float eps, hipStream_t stream) {
+    if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, x, ldx, gamma, beta,
+                       reinterpret_cast<bf16_t*>(out_bf16), ldb, out_f32, ldf, M, D, eps);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t dlms_layernorm_gather(const float* x, int ldx, const int* rows, const float* gamma,
+                                            const float* beta, void* out_bf16, int ldb, int M, int D, float eps,
+                                            hipStream_t stream) {
+    if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(layernorm_gather_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, x, ldx, rows, gamma, beta,
+                       reinterpret_cast<bf16_t*>(out_bf16), ldb, M, D, eps);
+    return hipGetLastError();
+}

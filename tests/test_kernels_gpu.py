@@ -1,0 +1,206 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op
+(SURVEY.md §4.3 "Kernel unit")."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from distributed_lms_raft_llm_amd import ops
+
+    ops.lib()
+    return ops
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (7, 192, 128), (16, 768, 768), (33, 2304, 768), (128, 3072, 768),
+                                   (130, 768, 3072), (300, 256, 512), (1000, 128, 64)])
+def test_gemm_bias_bf16(M, N, K):
+    ops = _ops()
+    a, w = _bf(M, K, seed=1), _bf(N, K, scale=0.05, seed=2)
+    bias = torch.randn(N, device=DEV)
+    out = ops.gemm(a, w, ops.EPI_BF16, bias=bias)
+    ref = a.float() @ w.float().t() + bias
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_gemm_asymmetric_identity():
+    # A = I with an asymmetric B catches a transposed C-write (cdna_hip_programming.md §3).
+    ops = _ops()
+    K = 64
+    a = torch.eye(K, device=DEV).to(torch.bfloat16)
+    w = torch.arange(K * 64, device=DEV, dtype=torch.float32).reshape(64, K).remainder(97).to(torch.bfloat16)
+    out = ops.gemm(a, w, ops.EPI_BF16)
+    torch.testing.assert_close(out.float(), w.float().t(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("epi", ["gelu_tanh", "gelu_erf"])
+def test_gemm_gelu(epi):
+    ops = _ops()
+    M, N, K = 96, 3072, 768
+    a, w = _bf(M, K, seed=3), _bf(N, K, scale=0.05, seed=4)
+    bias = torch.randn(N, device=DEV) * 0.1
+    e = ops.EPI_GELU_TANH if epi == "gelu_tanh" else ops.EPI_GELU_ERF
+    out = ops.gemm(a, w, e, bias=bias)
+    z = a.float() @ w.float().t() + bias
+    ref = torch.nn.functional.gelu(z, approximate="tanh" if epi == "gelu_tanh" else "none")
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_gemm_f32_residual_inplace():
+    ops = _ops()
+    M, N, K = 64, 768, 3072
+    a, w = _bf(M, K, seed=5), _bf(N, K, scale=0.02, seed=6)
+    bias = torch.randn(N, device=DEV)
+    x = torch.randn(M, N, device=DEV)
+    ref = x + a.float() @ w.float().t() + bias
+    ops.gemm(a, w, ops.EPI_F32, bias=bias, out=x, resid=x)
+    torch.testing.assert_close(x, ref, atol=1e-2, rtol=1e-3)
+
+
+def test_gemm_qkv_scatter():
+    ops = _ops()
+    H, T, S = 4, 16, 3
+    D = H * 64
+    M = 5
+    a, w = _bf(M, D, seed=7), _bf(3 * D, D, scale=0.05, seed=8)
+    bias = torch.randn(3 * D, device=DEV)
+    q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    slot = torch.tensor([0, 2, 2, 1, 0], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([3, 0, 7, 15, 4], dtype=torch.int32, device=DEV)
+    ops.gemm(a, w, ops.EPI_QKV, bias=bias, q_out=q, k_cache=kc, v_cache=vc, row_slot=slot, row_pos=pos)
+    ref = a.float() @ w.float().t() + bias
+    torch.testing.assert_close(q.float(), ref[:, :D], atol=2e-2, rtol=2e-2)
+    for m in range(M):
+        s, p = int(slot[m]), int(pos[m])
+        torch.testing.assert_close(kc[s, :, p].float().reshape(-1), ref[m, D:2 * D], atol=2e-2, rtol=2e-2)
+        torch.testing.assert_close(vc[s, :, p].float().reshape(-1), ref[m, 2 * D:], atol=2e-2, rtol=2e-2)
+
+
+def test_gemm_argmax_penalty():
+    ops = _ops()
+    M, K, V = 37, 768, 50257
+    Vp = (V + 63) // 64 * 64
+    a = _bf(M, K, seed=9)
+    w = torch.zeros(Vp, K, dtype=torch.bfloat16, device=DEV)
+    w[:V] = _bf(V, K, scale=0.05, seed=10)
+    seen = torch.zeros(M, Vp // 32, dtype=torch.int32, device=DEV)
+    logits = a.float() @ w.float().t()
+    # mark the current argmax (and some others) as seen so the penalty must change the answer
+    top = logits[:, :V].argmax(1)
+    seen_bool = torch.zeros(M, Vp, dtype=torch.bool, device=DEV)
+    seen_bool[torch.arange(M), top] = True
+    seen_bool[:, :500] = True
+    words = torch.zeros(M, Vp // 32, dtype=torch.int64, device=DEV)
+    for bit in range(32):
+        words |= seen_bool.view(M, Vp // 32, 32)[:, :, bit].long() << bit
+    seen.copy_(words.to(torch.int64).where(words < 2**31, words - 2**32).to(torch.int32))
+    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
+    ops.gemm(a, w, ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2)
+    pen = torch.where(logits < 0, logits * 1.2, logits / 1.2)
+    ref = torch.where(seen_bool, pen, logits)[:, :V]
+    got = (~(keys & 0xFFFFFFFF)).bitwise_and(0xFFFFFFFF)
+    ref_idx = ref.argmax(1)
+    # allow a different index only on a numerical near-tie
+    ok = (got == ref_idx) | ((ref.gather(1, got[:, None]).squeeze(1) - ref.max(1).values).abs() < 1e-3)
+    assert bool(ok.all()), (got, ref_idx)
+
+
+@pytest.mark.parametrize("M,D", [(1, 768), (5, 1024), (64, 1280), (33, 1600)])
+def test_layernorm(M, D):
+    ops = _ops()
+    x = torch.randn(M, D, device=DEV) * 3 + 1
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    of = torch.empty(M, D, device=DEV)
+    ob = ops.layernorm(x, g, b, 1e-5, out_f32=of)
+    ref = torch.nn.functional.layer_norm(x, (D,), g, b, 1e-5)
+    torch.testing.assert_close(of, ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ob.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("kvlens", [[1, 5, 150], [64, 63, 65, 1024]])
+def test_row_attention(kvlens):
+    ops = _ops()
+    H, T = 3, 1024
+    R = len(kvlens)
+    q = _bf(R, H * 64, seed=11)
+    kc = _bf(R, H, T, 64, seed=12)
+    vc = _bf(R, H, T, 64, seed=13)
+    slot = torch.arange(R, dtype=torch.int32, device=DEV).flip(0)
+    kvl = torch.tensor(kvlens, dtype=torch.int32, device=DEV)
+    out = ops.row_attention(q, kc, vc, slot, kvl)
+    for r in range(R):
+        s, L = int(slot[r]), kvlens[r]
+        qq = q[r].float().view(H, 64)
+        K = kc[s, :, :L].float()
+        V = vc[s, :, :L].float()
+        p = torch.softmax(torch.einsum("hd,htd->ht", qq, K) / 8.0, -1)
+        ref = torch.einsum("ht,htd->hd", p, V).reshape(-1)
+        torch.testing.assert_close(out[r].float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_embed_and_decode_update():
+    ops = _ops()
+    V, P, D, B, T = 1000, 64, 128, 3, 10
+    wte, wpe = _bf(V, D, seed=14), _bf(P, D, seed=15)
+    tok = torch.tensor([5, 999, 0], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 7, 63], dtype=torch.int32, device=DEV)
+    x = ops.embed(tok, pos, wte, wpe)
+    torch.testing.assert_close(x, wte[tok.long()].float() + wpe[pos.long()].float())
+
+    keys = torch.zeros(B, dtype=torch.int64, device=DEV)
+    # row 0 -> token 17, row 1 -> eos (999), row 2 already finished
+    def key(v, i):
+        u = torch.tensor([v], dtype=torch.float32).view(torch.int32).item() & 0xFFFFFFFF
+        o = (~u & 0xFFFFFFFF) if (u & 0x80000000) else (u | 0x80000000)
+        k = (o << 32) | (~i & 0xFFFFFFFF)
+        return k - (1 << 64) if k >= (1 << 63) else k
+    keys.copy_(torch.tensor([key(1.5, 17), key(-2.0, 999), key(0.0, 3)], dtype=torch.int64))
+    lens = torch.tensor([4, 9, 10], dtype=torch.int32, device=DEV)
+    fin = torch.tensor([0, 0, 1], dtype=torch.int32, device=DEV)
+    out = torch.zeros(B, T, dtype=torch.int32, device=DEV)
+    out[2, 9] = 42
+    seen = torch.zeros(B, 32, dtype=torch.int32, device=DEV)
+    ct, cp, ck = (torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(3))
+    xb = torch.zeros(B, D, device=DEV)
+    ops.decode_update(keys, keys, lens, fin, out, seen, ct, cp, ck, wte, wpe, xb, eos=999, t_max=T)
+    assert lens.tolist() == [5, 10, 10]
+    assert fin.tolist() == [0, 1, 1]
+    assert out[0, 4].item() == 17 and out[1, 9].item() == 999
+    assert ct.tolist() == [17, 999, 42] and cp.tolist() == [4, 9, 9] and ck.tolist() == [5, 10, 10]
+    assert keys.tolist() == [0, 0, 0]
+    assert (seen[0, 0].item() >> 17) & 1 == 1
+    torch.testing.assert_close(xb[0], wte[17].float() + wpe[4].float())
+
+
+def test_bert_embed_pool_cosine():
+    ops = _ops()
+    V, P, D = 100, 32, 128
+    word = torch.randn(V, D, device=DEV)
+    pe = torch.randn(P, D, device=DEV)
+    t0 = torch.randn(D, device=DEV)
+    g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    ids = torch.tensor([1, 5, 7, 9, 2], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 1, 2, 0, 1], dtype=torch.int32, device=DEV)
+    xf, xb = ops.bert_embed_ln(ids, pos, word, pe, t0, g, b, 1e-12)
+    ref = torch.nn.functional.layer_norm(word[ids.long()] + pe[pos.long()] + t0, (D,), g, b, 1e-12)
+    torch.testing.assert_close(xf, ref, atol=1e-4, rtol=1e-4)
+    start = torch.tensor([0, 3], dtype=torch.int32, device=DEV)
+    ln = torch.tensor([3, 2], dtype=torch.int32, device=DEV)
+    pooled = ops.mean_pool(xf, start, ln)
+    torch.testing.assert_close(pooled, torch.stack([ref[:3].mean(0), ref[3:].mean(0)]), atol=1e-5, rtol=1e-5)
+    sim = ops.cosine(pooled, pooled)
+    refsim = torch.nn.functional.cosine_similarity(pooled[:, None], pooled[None], dim=-1)
+    torch.testing.assert_close(sim, refsim, atol=1e-5, rtol=1e-5)
