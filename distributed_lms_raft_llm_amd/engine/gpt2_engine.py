@@ -103,7 +103,7 @@ class HipGPT2Engine:
         # KV cache [L][2][slots][H_local][T][64]: sized for the batch at full length.
         self.kv = torch.zeros(cfg.n_layer, 2, B, Hl, T, 64, dtype=bf, device=dev)
         self.x = torch.zeros(B, D, dtype=f32, device=dev)
-        self.y = torch.zeros(B, D, dtype=f32, device=dev)
+        self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
         self.h = torch.zeros(B, D, dtype=bf, device=dev)
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.att = torch.zeros(B, Dl, dtype=bf, device=dev)
@@ -141,33 +141,51 @@ class HipGPT2Engine:
         return self.local_keys[:B]
 
     # ------------------------------------------------------------------ transformer body
-    def _layers(self, x: torch.Tensor, y: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int):
-        """Run all blocks on rows [0, M) of the residual ``x`` (in place; ``y`` is TP scratch)."""
+    def _split(self, M: int, N: int, K: int) -> int:
+        """Split-K factor for a row-parallel projection (N = d): decode GEMMs are latency-bound, so
+        slice K until the grid covers the CUs, keeping >= 3 K-steps per slice."""
+        if self.tp_size > 1 or M > 512:
+            return 1
+        bm = 16 if M <= 16 else 32 if M <= 32 else 64
+        tiles = -(-M // bm) * (N // 64)
+        ksteps = K // 64
+        best = 1
+        for s in (2, 3, 4, 6, 8):
+            if ksteps % s == 0 and tiles * s <= 512 and ksteps // s >= 3:
+                best = s
+        return best
+
+    def _row_parallel(self, a: torch.Tensor, w: torch.Tensor, bias, parts: torch.Tensor, M: int):
+        """out-proj / c_proj: split-K (TP=1) or TP partial + all-reduce.  Returns the pending
+        residual update (parts, nsplit, bias) that the next fused add+LayerNorm applies."""
+        if self.tp_size > 1:
+            ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=1)
+            self._all_reduce(parts[0, :M])
+            return parts, 1, bias
+        s = self._split(M, w.shape[0], w.shape[1])
+        ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=s)
+        return parts, s, bias
+
+    def _layers(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
+                final_h: torch.Tensor | None):
+        """All blocks on rows [0, M) of the residual ``x`` (updated in place), then ln_f into
+        ``final_h`` (or only the last residual update when ``final_h`` is None)."""
         w, cfg = self.w, self.cfg
         eps = cfg.layer_norm_epsilon
-        tp = self.tp_size > 1
         xs, hs, qs, ats, ffs = x[:M], h[:M], q[:M], att[:M], ff[:M]
-        ys = y[:M]
+        pend = (None, 0, None)
         for li, lw in enumerate(w.layers):
             kc, vc = self.kv[li, 0], self.kv[li, 1]
-            ops.layernorm(xs, lw.ln1_g, lw.ln1_b, eps, out_bf16=hs)
+            ops.add_layernorm(xs, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], out_bf16=hs)
             ops.gemm(hs, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
                      row_slot=row_slot, row_pos=row_pos)
             ops.row_attention(qs, kc, vc, row_slot, row_kvlen, out=ats)
-            if tp:
-                ops.gemm(ats, lw.w_o, ops.EPI_F32, bias=lw.b_o, out=ys, resid=xs if self.tp_rank == 0 else None)
-                self._all_reduce(ys)
-                res = ys
-            else:
-                ops.gemm(ats, lw.w_o, ops.EPI_F32, bias=lw.b_o, out=xs, resid=xs)
-                res = xs
-            ops.layernorm(res, lw.ln2_g, lw.ln2_b, eps, out_bf16=hs)
+            pend = self._row_parallel(ats, lw.w_o, lw.b_o, parts, M)
+            ops.add_layernorm(xs, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], out_bf16=hs)
             ops.gemm(hs, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs)
-            if tp:
-                ops.gemm(ffs, lw.w_p, ops.EPI_F32, bias=lw.b_p, out=xs, resid=ys if self.tp_rank == 0 else None)
-                self._all_reduce(xs)
-            else:
-                ops.gemm(ffs, lw.w_p, ops.EPI_F32, bias=lw.b_p, out=xs, resid=xs)
+            pend = self._row_parallel(ffs, lw.w_p, lw.b_p, parts, M)
+        ops.add_layernorm(xs, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], out_bf16=final_h,
+                          want_out=final_h is not None)
 
     def _lm_head_and_update(self, hidden_bf16: torch.Tensor, B: int, penalty: float):
         cfg = self.cfg
@@ -179,9 +197,8 @@ class HipGPT2Engine:
                           self.w.wpe, self.x[:B], cfg.eos_token_id, self.max_length)
 
     def _decode_step(self, B: int, penalty: float):
-        self._layers(self.x, self.y, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
-                     self.cur_kvlen[:B], B)
-        ops.layernorm(self.x[:B], self.w.lnf_g, self.w.lnf_b, self.cfg.layer_norm_epsilon, out_bf16=self.h[:B])
+        self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
+                     self.cur_kvlen[:B], B, final_h=self.h[:B])
         self._lm_head_and_update(self.h[:B], B, penalty)
 
     def _graph_for(self, B: int, penalty: float) -> torch.cuda.CUDAGraph:
@@ -248,12 +265,13 @@ class HipGPT2Engine:
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         f32, bf = torch.float32, torch.bfloat16
         x = ops.embed(tokens_d, pos_d, self.w.wte, self.w.wpe)
-        y = torch.empty(R, D, dtype=f32, device=dev) if self.tp_size > 1 else x
+        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl))
+        parts = torch.empty(nsplit, R, D, dtype=f32, device=dev)
         h = torch.empty(R, D, dtype=bf, device=dev)
         q = torch.empty(R, Dl, dtype=bf, device=dev)
         att = torch.empty(R, Dl, dtype=bf, device=dev)
         ff = torch.empty(R, Fl, dtype=bf, device=dev)
-        self._layers(x, y, h, q, att, ff, slot_d, pos_d, kvlen_d, R)
+        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, kvlen_d, R, final_h=None)
         hl = ops.layernorm_gather(x, last_d, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon)
         self._lm_head_and_update(hl, B, penalty)
 
@@ -269,10 +287,11 @@ class HipGPT2Engine:
         last = torch.tensor([sum(lens[: b + 1]) - 1 for b in range(len(prompts))], dtype=torch.int32, device=dev)
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         x = ops.embed(tokens, pos, self.w.wte, self.w.wpe)
-        y = torch.empty(R, D, device=dev) if self.tp_size > 1 else x
+        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl))
+        parts = torch.empty(nsplit, R, D, device=dev)
         bf = torch.bfloat16
         h, q, att, ff = (torch.empty(R, n, dtype=bf, device=dev) for n in (D, Dl, Dl, Fl))
-        self._layers(x, y, h, q, att, ff, slot, pos, pos + 1, R)
+        self._layers(x, parts, h, q, att, ff, slot, pos, pos + 1, R, final_h=None)
         return ops.layernorm_gather(x, last, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon).float()
 
     # ------------------------------------------------------------------ public API

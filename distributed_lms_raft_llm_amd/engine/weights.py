@@ -10,8 +10,9 @@ parameters stay fp32.  TP sharding:
 * LM head: vocab-parallel over the tied ``wte`` (shard boundaries on 64-row tiles) with a
   fused local argmax and a cross-rank (value, index) max.
 
-Row-parallel biases live on rank 0 only, so the all-reduce of the partial sums yields exactly
-``x + bias + sum(partials)``.
+Row-parallel GEMMs emit raw fp32 partials; after the all-reduce every rank applies
+``x += bias + sum(partials)`` in the fused add+LayerNorm kernel, so the replicated residual stays
+bit-identical across ranks.
 """
 from __future__ import annotations
 
@@ -40,13 +41,13 @@ class LayerWeights:
     w_qkv: torch.Tensor  # [3*Dl, D]
     b_qkv: torch.Tensor  # [3*Dl]
     w_o: torch.Tensor  # [D, Dl]
-    b_o: torch.Tensor | None  # [D] on rank 0
+    b_o: torch.Tensor  # [D], added once after the reduction
     ln2_g: torch.Tensor
     ln2_b: torch.Tensor
     w_fc: torch.Tensor  # [Fl, D]
     b_fc: torch.Tensor  # [Fl]
     w_p: torch.Tensor  # [D, Fl]
-    b_p: torch.Tensor | None  # [D] on rank 0
+    b_p: torch.Tensor  # [D], added once after the reduction
 
 
 @dataclass
@@ -125,9 +126,9 @@ def prepare_gpt2_weights(cfg: GPT2Config, w: dict[str, torch.Tensor], device, tp
         out.layers.append(LayerWeights(
             ln1_g=dev(w[p + "ln_1.weight"], f32), ln1_b=dev(w[p + "ln_1.bias"], f32),
             w_qkv=dev(w_qkv), b_qkv=dev(b_qkv, f32),
-            w_o=dev(wo), b_o=dev(w[p + "attn.c_proj.bias"], f32) if tp_rank == 0 else None,
+            w_o=dev(wo), b_o=dev(w[p + "attn.c_proj.bias"], f32),
             ln2_g=dev(w[p + "ln_2.weight"], f32), ln2_b=dev(w[p + "ln_2.bias"], f32),
             w_fc=dev(wfc), b_fc=dev(w[p + "mlp.c_fc.bias"].float()[f0:f1], f32),
-            w_p=dev(wp), b_p=dev(w[p + "mlp.c_proj.bias"], f32) if tp_rank == 0 else None,
+            w_p=dev(wp), b_p=dev(w[p + "mlp.c_proj.bias"], f32),
         ))
     return out

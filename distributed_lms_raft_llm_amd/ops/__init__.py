@@ -28,7 +28,7 @@ LIB_PATH = LIB_DIR / "libdlms_hip.so"
 SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
-EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX = range(6)
+EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
 
 _lock = threading.Lock()
 _lib = None
@@ -75,6 +75,7 @@ class GemmEpi(ctypes.Structure):
         ("argmax_out", ctypes.c_void_p), ("seen", ctypes.c_void_p),
         ("seen_words", ctypes.c_int), ("vocab", ctypes.c_int), ("col_offset", ctypes.c_int),
         ("penalty", ctypes.c_float),
+        ("split_k", ctypes.c_int), ("split_stride", ctypes.c_longlong),
     ]
 
 
@@ -84,6 +85,7 @@ def _bind(L):
         "dlms_gemm": [I, P, I, P, I, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_layernorm": [P, I, P, P, P, I, P, I, I, I, F, P],
         "dlms_layernorm_gather": [P, I, P, P, P, P, I, I, I, F, P],
+        "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, I, I, F, P],
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
         "dlms_decode_update": [P, I, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I, I, P],
@@ -153,7 +155,8 @@ def _req(t: torch.Tensor, dtype, name: str, dim: int | None = None):
 # ---------------------------------------------------------------------------------------------
 def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, out=None, resid=None,
          q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
-         argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0):
+         argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0,
+         split_k: int = 1):
     """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0)."""
     _req(a, torch.bfloat16, "a", 2)
     _req(w, torch.bfloat16, "w", 2)
@@ -199,6 +202,15 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
         ep.n_heads, ep.t_max, ep.d_local = k_cache.shape[1], k_cache.shape[2], d_local
         out = q_out
+    elif epi == EPI_PARTIAL:
+        if split_k < 1 or K % (64 * split_k):
+            raise ValueError(f"split_k={split_k} must divide K/64 (K={K})")
+        if out is None:
+            out = torch.empty(split_k, M, N, dtype=torch.float32, device=a.device)
+        _req(out, torch.float32, "out", 3)
+        if out.shape[0] < split_k or out.shape[1] < M or out.shape[2] < N:
+            raise ValueError("partial out too small")
+        ep.out, ep.ldo, ep.split_k, ep.split_stride = out.data_ptr(), out.stride(1), split_k, out.stride(0)
     elif epi == EPI_ARGMAX:
         _req(argmax_out, torch.int64, "argmax_out", 1)
         _req(seen, torch.int32, "seen", 2)
@@ -237,6 +249,36 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
                                 out_f32.stride(0) if out_f32 is not None else 0, M, D, float(eps), _stream()),
            "dlms_layernorm")
     return out_bf16 if out_bf16 is not None else out_f32
+
+
+def add_layernorm(x: torch.Tensor, gamma, beta, eps: float, *, parts: torch.Tensor | None = None, nsplit: int = 0,
+                  bias: torch.Tensor | None = None, out_bf16: torch.Tensor | None = None, want_out: bool = True):
+    """x += bias + sum(parts[:nsplit]) (in place), then out = bf16(LN(x)).  parts: f32 [S, >=M, >=D]."""
+    _req(x, torch.float32, "x", 2)
+    M, D = x.shape
+    if D % 4 or D > 2048 or gamma.numel() != D or beta.numel() != D:
+        raise ValueError("add_layernorm: bad D/gamma/beta")
+    ldp, sstride = 0, 0
+    if nsplit:
+        _req(parts, torch.float32, "parts", 3)
+        if parts.shape[0] < nsplit or parts.shape[1] < M or parts.shape[2] < D:
+            raise ValueError("add_layernorm: parts too small")
+        ldp, sstride = parts.stride(1), parts.stride(0)
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() != D:
+            raise ValueError("add_layernorm: bias size")
+    if want_out and out_bf16 is None:
+        out_bf16 = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+    if out_bf16 is not None:
+        _req(out_bf16, torch.bfloat16, "out_bf16", 2)
+        if out_bf16.shape[0] < M or out_bf16.shape[1] < D:
+            raise ValueError("add_layernorm: out too small")
+    _check(lib().dlms_add_layernorm(_p(x), x.stride(0), _p(parts) if nsplit else None, ldp, sstride, nsplit,
+                                    _p(bias), _p(gamma), _p(beta), _p(out_bf16),
+                                    out_bf16.stride(0) if out_bf16 is not None else 0, M, D, float(eps), _stream()),
+           "dlms_add_layernorm")
+    return out_bf16
 
 
 def layernorm_gather(x: torch.Tensor, rows: torch.Tensor, gamma, beta, eps: float, out_bf16=None):

@@ -124,4 +124,8 @@ struct GemmEpi {
     int vocab;       // number of valid global vocab ids
     int col_offset;  // global id of local column 0 (vocab-parallel shards)
     float penalty;
+    // split-K (EPI_PARTIAL): the grid carries split_k K-slices; slice s writes its fp32 partial tile
+    // at out + s * split_stride (elements).  Summed later by the fused add+LayerNorm kernel.
+    int split_k;
+    long long split_stride;
 };

@@ -5,8 +5,8 @@
 // A is the activation (row-major, K contiguous), W the weight stored [N][K] (K contiguous) so
 // that both MFMA operands are read as contiguous 16-byte fragments.  One workgroup = 4 waves
 // (256 threads) computes a BM x BN tile with v_mfma_f32_16x16x32_bf16; K advances in 64-deep
-// steps staged through a double-buffered, padded LDS image (one barrier per K-step, the next
-// step's global loads in flight behind the current step's MFMAs).
+// steps through a 3-stage LDS ring filled by LDS-DMA (two steps of loads in flight behind the
+// MFMAs of the current one, one raw barrier per step).
 //
 // Epilogues (all fused, no extra pass over C):
 //   EPI_BF16        out = bf16(acc + bias)
@@ -16,16 +16,36 @@
 //                                                                in-place when out == resid
 //   EPI_QKV         q -> q_out, k/v scattered into the KV cache at (slot,pos) of each row (K3+K4)
 //   EPI_ARGMAX      repetition-penalised logits -> per-row packed (value,index) atomicMax (K10-K12)
+//   EPI_PARTIAL     split-K: slice s stores its raw fp32 partial tile; the following fused
+//                   residual-add + LayerNorm kernel sums the slices in a fixed order (deterministic,
+//                   no atomics) -- the decode projections with N = d are split 2-4 ways so the
+//                   latency-bound skinny GEMMs put enough workgroups on the 256 CUs.
 #include "common.h"
 
-enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5 };
+enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6 };
 
 // struct GemmEpi lives in common.h (shared with the ABI probe in api.hip)
 
 #define GEMM_BK 64
-#define GEMM_LDS_STRIDE (GEMM_BK + 8)  // +16 B pad per row breaks the 128-B row bank aliasing
 
-template <int BM, int BN, int WM, int WN, int EPI>
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Main loop: K advances in 64-deep steps through a STAGES-deep LDS ring (STAGES-1 steps of loads in
+// flight: the decode GEMMs are HBM-latency-bound, so the ring is as deep as the LDS allows) filled by
+// global_load_lds_dwordx4 (LDS-DMA, no staging registers).  Each 1-KiB wave-instruction lands 8 tile
+// rows of 128 B; the 16-B chunks of a row are XOR-swizzled (phys = logical ^ (row & 7)) by permuting
+// the per-lane SOURCE address, and the fragment reads apply the same involution, which makes the
+// ds_read_b128 fragment loads bank-conflict free (cdna_hip_programming.md rule 21 / T2).
+// Synchronisation: counted `s_waitcnt vmcnt` + raw s_barrier (a __syncthreads() would drain the
+// in-flight DMA every step); out-of-range A rows read a clamped valid row (their results are never
+// stored), so the DMA never needs predication.
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__ A, int lda,
                                                       const bf16_t* __restrict__ W, int ldw, int M, int N,
                                                       int K, GemmEpi ep) {
@@ -35,14 +55,14 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
     constexpr int TM = WTM / 16;
     constexpr int TN = WTN / 16;
     static_assert(TM >= 1 && TN >= 1, "wave tile must hold at least one 16x16 MFMA tile");
-    constexpr int A_CHUNKS = BM * GEMM_BK / 8;  // 16-byte chunks per A tile
-    constexpr int W_CHUNKS = BN * GEMM_BK / 8;
-    constexpr int A_PER_T = (A_CHUNKS + 255) / 256;
-    constexpr int W_PER_T = (W_CHUNKS + 255) / 256;
+    constexpr int ROWB = GEMM_BK * 2;  // 128 B per tile row
+    constexpr int A_BYTES = BM * ROWB;
+    constexpr int STAGE_BYTES = (BM + BN) * ROWB;
+    constexpr int PIECES = STAGE_BYTES / 1024;
+    static_assert(PIECES % 4 == 0, "(BM + BN) must be a multiple of 32");
+    constexpr int PPW = PIECES / 4;  // LDS-DMA instructions per wave per stage
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t* As = reinterpret_cast<bf16_t*>(smem);                     // [2][BM][STRIDE]
-    bf16_t* Ws = As + 2 * BM * GEMM_LDS_STRIDE;                        // [2][BN][STRIDE]
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -52,54 +72,38 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
 
     const int tiles_m = (M + BM - 1) / BM;
     const int nwg = gridDim.x;
-    const int bid = xcd_remap(blockIdx.x, nwg);
+    const int nsplit = EPI == EPI_PARTIAL ? ep.split_k : 1;
+    const int tiles = nwg / nsplit;
+    const int bid0 = xcd_remap(blockIdx.x, nwg);
+    const int split = bid0 / tiles;
+    const int bid = bid0 - split * tiles;
     const int tile_m = bid % tiles_m;
     const int tile_n = bid / tiles_m;
     const int m0 = tile_m * BM;
     const int n0 = tile_n * BN;
+    const int k_len = K / nsplit;
+    const int k_base = split * k_len;
 
-    uint4 ra[A_PER_T];
-    uint4 rw[W_PER_T];
-
-    auto load_tile = [&](int k0) {
+    // per-lane DMA sources (fixed for the K loop)
+    const bf16_t* src[PPW];
 #pragma unroll
-        for (int i = 0; i < A_PER_T; ++i) {
-            const int c = tid + i * 256;
-            if (c < A_CHUNKS) {
-                const int r = c >> 3, kc = c & 7;
-                const int gm = m0 + r;
-                ra[i] = (gm < M) ? *reinterpret_cast<const uint4*>(A + (size_t)gm * lda + k0 + kc * 8)
-                                 : make_uint4(0, 0, 0, 0);
-            }
+    for (int i = 0; i < PPW; ++i) {
+        const int piece = wave + 4 * i;
+        const int row = piece * 8 + (lane >> 3);
+        const int lchunk = (lane & 7) ^ (lane >> 3);
+        if (row < BM) {
+            const int gm = m0 + row < M ? m0 + row : M - 1;
+            src[i] = A + (size_t)gm * lda + k_base + lchunk * 8;
+        } else {
+            src[i] = W + (size_t)(n0 + row - BM) * ldw + k_base + lchunk * 8;
         }
+    }
+    auto issue = [&](int stage, int k0) {
+        char* dst = smem + stage * STAGE_BYTES;
 #pragma unroll
-        for (int i = 0; i < W_PER_T; ++i) {
-            const int c = tid + i * 256;
-            if (c < W_CHUNKS) {
-                const int r = c >> 3, kc = c & 7;
-                rw[i] = *reinterpret_cast<const uint4*>(W + (size_t)(n0 + r) * ldw + k0 + kc * 8);
-            }
-        }
-    };
-    auto store_tile = [&](int buf) {
-        bf16_t* as = As + buf * BM * GEMM_LDS_STRIDE;
-        bf16_t* ws = Ws + buf * BN * GEMM_LDS_STRIDE;
-#pragma unroll
-        for (int i = 0; i < A_PER_T; ++i) {
-            const int c = tid + i * 256;
-            if (c < A_CHUNKS) {
-                const int r = c >> 3, kc = c & 7;
-                *reinterpret_cast<uint4*>(as + r * GEMM_LDS_STRIDE + kc * 8) = ra[i];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < W_PER_T; ++i) {
-            const int c = tid + i * 256;
-            if (c < W_CHUNKS) {
-                const int r = c >> 3, kc = c & 7;
-                *reinterpret_cast<uint4*>(ws + r * GEMM_LDS_STRIDE + kc * 8) = rw[i];
-            }
-        }
+        for (int i = 0; i < PPW; ++i)
+            __builtin_amdgcn_global_load_lds((glob_void_t*)(src[i] + k0), (lds_void_t*)(dst + (wave + 4 * i) * 1024),
+                                             16, 0, 0);
     };
 
     f32x4_t acc[TM][TN];
@@ -108,37 +112,50 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-    const int nk = K / GEMM_BK;
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
+    const int nk = k_len / GEMM_BK;
+    // prologue: up to STAGES-1 steps in flight; no step is ever loaded twice (short split-K slices
+    // would otherwise multiply their traffic)
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) issue(s, s * GEMM_BK);
 
-    const int frag_row = lane & 15;
-    const int frag_k = (lane >> 4) * 8;
+    const int frow = lane & 15;
+    const int fk = lane >> 4;
+    const int fsw = lane & 7;  // == row & 7 for every fragment row this lane reads
 
     for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load_tile((kt + 1) * GEMM_BK);
-        const bf16_t* as = As + buf * BM * GEMM_LDS_STRIDE + (wm * WTM) * GEMM_LDS_STRIDE;
-        const bf16_t* ws = Ws + buf * BN * GEMM_LDS_STRIDE + (wn * WTN) * GEMM_LDS_STRIDE;
+        // this lane's share of step kt has landed (steady state: STAGES-2 younger steps may stay in
+        // flight; in the tail fewer were issued, so drain everything) ...
+        if (nk - kt >= STAGES - 1)
+            wait_vmcnt<(STAGES - 2) * PPW>();
+        else
+            wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // ... and every other lane's; all reads of step kt-1 are done
+        asm volatile("" ::: "memory");
+        {
+            const int kn = kt + STAGES - 1;
+            if (kn < nk) issue(kn % STAGES, kn * GEMM_BK);
+        }
+        const char* as = smem + (kt % STAGES) * STAGE_BYTES + (wm * WTM) * ROWB;
+        const char* ws = smem + (kt % STAGES) * STAGE_BYTES + A_BYTES + (wn * WTN) * ROWB;
 #pragma unroll
         for (int ks = 0; ks < GEMM_BK / 32; ++ks) {
+            const int coff = (((ks * 4 + fk) ^ fsw) << 4);
             bf16x8_t af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                af[i] = *reinterpret_cast<const bf16x8_t*>(as + (i * 16 + frag_row) * GEMM_LDS_STRIDE + ks * 32 + frag_k);
+                af[i] = *reinterpret_cast<const bf16x8_t*>(as + (i * 16 + frow) * ROWB + coff);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bfr[j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frag_row) * GEMM_LDS_STRIDE + ks * 32 + frag_k);
+                bfr[j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frow) * ROWB + coff);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) store_tile(buf ^ 1);
-        __syncthreads();
     }
+    wait_vmcnt<0>();  // drain the tail DMA before the workgroup may exit / LDS be reused
 
     // ---------------- epilogue ----------------
     // accumulator element r of tile (i,j): row = (lane>>4)*4 + r, col = lane & 15
@@ -191,7 +208,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int col = col_base + j * 16;
-        const float bv = ep.bias ? ep.bias[col] : 0.f;
+        const float bv = (EPI != EPI_PARTIAL && ep.bias) ? ep.bias[col] : 0.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -208,6 +225,9 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
                 } else if constexpr (EPI == EPI_F32) {
                     if (ep.resid) v += ep.resid[(size_t)row * ep.ldr + col];
                     reinterpret_cast<float*>(ep.out)[(size_t)row * ep.ldo + col] = v;
+                } else if constexpr (EPI == EPI_PARTIAL) {
+                    reinterpret_cast<float*>(ep.out)[(size_t)split * ep.split_stride + (size_t)row * ep.ldo + col] =
+                        acc[i][j][r];
                 } else if constexpr (EPI == EPI_QKV) {
                     const int part = col / ep.d_local;
                     const int within = col - part * ep.d_local;
@@ -226,34 +246,42 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
     }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
 static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
-    const int tiles = ((M + BM - 1) / BM) * (N / BN);
-    const size_t lds = (size_t)2 * (BM + BN) * GEMM_LDS_STRIDE * sizeof(bf16_t);
-    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, EPI>), dim3(tiles), dim3(256), lds, stream, A, lda, W, ldw, M,
-                       N, K, ep);
+    const int tiles = ((M + BM - 1) / BM) * (N / BN) * (EPI == EPI_PARTIAL ? ep.split_k : 1);
+    const size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * sizeof(bf16_t);
+    static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI>), dim3(tiles), dim3(256), lds, stream, A, lda, W,
+                       ldw, M, N, K, ep);
     return hipGetLastError();
 }
 
-// Tile selection: decode GEMMs (M = live batch) are latency-bound, so favour enough workgroups
-// to cover the 256 CUs; prefill/encoder GEMMs (M in the thousands) take 128x64 tiles.
+// Tile selection.  Decode GEMMs (M = live batch <= 256) are latency-bound: prefer the tile count
+// that covers the 256 CUs; prefill / encoder / LM-head GEMMs take 128-wide tiles (less operand
+// re-reading per MFMA).
 template <int EPI>
 static hipError_t launch_gemm_epi(const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
-    if (M <= 16) {
-        if (N % 64 == 0) return launch_gemm_cfg<16, 64, 1, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-        return launch_gemm_cfg<16, 64, 1, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    }
-    if (M <= 32) return launch_gemm_cfg<32, 64, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    const long tiles64 = (long)((M + 63) / 64) * (N / 64);
-    if (M <= 256 || tiles64 < 512) return launch_gemm_cfg<64, 64, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    return launch_gemm_cfg<128, 64, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    const int split = EPI == EPI_PARTIAL ? ep.split_k : 1;
+    if (M <= 32) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    const long t128x128 = (long)((M + 127) / 128) * (N / 128) * split;
+    const long t128x64 = (long)((M + 127) / 128) * (N / 64) * split;
+    if (N % 128 == 0 && t128x128 >= 256) return launch_gemm_cfg<128, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (t128x64 >= 256) return launch_gemm_cfg<128, 64, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
 }
 
 extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                 const GemmEpi* ep, hipStream_t stream) {
     if (K % GEMM_BK != 0 || N % 64 != 0 || M <= 0) return hipErrorInvalidValue;
+    if (epi == EPI_PARTIAL && (ep->split_k < 1 || K % (ep->split_k * GEMM_BK) != 0)) return hipErrorInvalidValue;
     const bf16_t* a = reinterpret_cast<const bf16_t*>(A);
     const bf16_t* w = reinterpret_cast<const bf16_t*>(W);
     switch (epi) {
@@ -263,6 +291,7 @@ extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, 
         case EPI_F32: return launch_gemm_epi<EPI_F32>(a, lda, w, ldw, M, N, K, *ep, stream);
         case EPI_QKV: return launch_gemm_epi<EPI_QKV>(a, lda, w, ldw, M, N, K, *ep, stream);
         case EPI_ARGMAX: return launch_gemm_epi<EPI_ARGMAX>(a, lda, w, ldw, M, N, K, *ep, stream);
+        case EPI_PARTIAL: return launch_gemm_epi<EPI_PARTIAL>(a, lda, w, ldw, M, N, K, *ep, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -119,3 +119,91 @@ extern "C" hipError_t dlms_layernorm_gather(const float* x, int ldx, const int* 
                        reinterpret_cast<bf16_t*>(out_bf16), ldb, M, D, eps);
     return hipGetLastError();
 }
+
+// Fused residual update + LayerNorm (one wave per row, 64-thread workgroups so a decode batch of
+// B rows spreads over B CUs):
+//     v = x + bias + sum_{s < nsplit} parts[s]      (fixed summation order: deterministic)
+//     x = v            (when anything was added)
+//     out = bf16(LN(v) * gamma + beta)               (skipped when out == nullptr)
+// This consumes the split-K partial slabs of the previous projection GEMM (EPI_PARTIAL) or, under
+// tensor parallelism, the all-reduced partial, so no GEMM epilogue ever read-modify-writes x.
+template <int NSPLIT>
+__global__ __launch_bounds__(64) void add_layernorm_kernel(float* x, int ldx, const float* __restrict__ parts,
+                                                           int ldp, long long split_stride,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, bf16_t* out, int ldb,
+                                                           int M, int D, float eps) {
+    const int lane = threadIdx.x;
+    const int row = blockIdx.x;
+    if (row >= M) return;
+    const int nv = D >> 2;
+    float4* xr = reinterpret_cast<float4*>(x + (size_t)row * ldx);
+    const bool update = NSPLIT > 0 || bias != nullptr;
+    float4 v[LN_MAX_V4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            float4 a = xr[c];
+            if (bias) {
+                const float4 b = reinterpret_cast<const float4*>(bias)[c];
+                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            }
+#pragma unroll
+            for (int k = 0; k < NSPLIT; ++k) {
+                const float4 p = reinterpret_cast<const float4*>(parts + (size_t)k * split_stride + (size_t)row * ldp)[c];
+                a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+            }
+            if (update) xr[c] = a;
+            v[i] = a;
+        } else {
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    if (out == nullptr) return;
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+            ss += (a * a + b * b) + (cc * cc + d * d);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+    const float4* g4 = reinterpret_cast<const float4*>(gamma);
+    const float4* b4 = reinterpret_cast<const float4*>(beta);
+#pragma unroll
+    for (int i = 0; i < LN_MAX_V4; ++i) {
+        const int c = lane + i * 64;
+        if (c < nv) {
+            const float4 g = g4[c], b = b4[c];
+            uint2 p;
+            p.x = pack_bf16x2((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y);
+            p.y = pack_bf16x2((v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+            reinterpret_cast<uint2*>(out + (size_t)row * ldb)[c] = p;
+        }
+    }
+}
+
+extern "C" hipError_t dlms_add_layernorm(float* x, int ldx, const float* parts, int ldp, long long split_stride,
+                                         int nsplit, const float* bias, const float* gamma, const float* beta,
+                                         void* out_bf16, int ldb, int M, int D, float eps, hipStream_t stream) {
+    if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0 || nsplit < 0 || nsplit > 8) return hipErrorInvalidValue;
+    bf16_t* o = reinterpret_cast<bf16_t*>(out_bf16);
+#define ADD_LN_CASE(NS)                                                                                       \
+    case NS:                                                                                                  \
+        hipLaunchKernelGGL(add_layernorm_kernel<NS>, dim3(M), dim3(64), 0, stream, x, ldx, parts, ldp, split_stride, \
+                           bias, gamma, beta, o, ldb, M, D, eps);                                             \
+        break;
+    switch (nsplit) {
+        ADD_LN_CASE(0) ADD_LN_CASE(1) ADD_LN_CASE(2) ADD_LN_CASE(3) ADD_LN_CASE(4) ADD_LN_CASE(5) ADD_LN_CASE(6)
+        ADD_LN_CASE(7) ADD_LN_CASE(8)
+    }
+#undef ADD_LN_CASE
+    return hipGetLastError();
+}

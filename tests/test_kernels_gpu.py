@@ -204,3 +204,33 @@ def test_bert_embed_pool_cosine():
     sim = ops.cosine(pooled, pooled)
     refsim = torch.nn.functional.cosine_similarity(pooled[:, None], pooled[None], dim=-1)
     torch.testing.assert_close(sim, refsim, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(256, 768, 3072, 4), (7, 768, 768, 3), (64, 256, 512, 8), (300, 128, 128, 1)])
+def test_gemm_split_k_partials_and_add_layernorm(M, N, K, S):
+    ops = _ops()
+    a, w = _bf(M, K, seed=21), _bf(N, K, scale=0.05, seed=22)
+    parts = torch.full((S, M, N), float("nan"), device=DEV)
+    ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=S)
+    full = a.float() @ w.float().t()
+    torch.testing.assert_close(parts.sum(0), full, atol=2e-3, rtol=1e-3)
+    # fused residual update + LayerNorm consumes the slabs
+    x = torch.randn(M, N, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    g, b = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
+    ref_x = x + bias + full
+    out = ops.add_layernorm(x, g, b, 1e-5, parts=parts, nsplit=S, bias=bias)
+    torch.testing.assert_close(x, ref_x, atol=2e-3, rtol=1e-3)
+    ref = torch.nn.functional.layer_norm(ref_x, (N,), g, b, 1e-5)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+def test_add_layernorm_no_update():
+    ops = _ops()
+    x = torch.randn(5, 768, device=DEV)
+    x0 = x.clone()
+    g, b = torch.randn(768, device=DEV), torch.randn(768, device=DEV)
+    out = ops.add_layernorm(x, g, b, 1e-5)
+    assert torch.equal(x, x0)
+    torch.testing.assert_close(out.float(), torch.nn.functional.layer_norm(x0, (768,), g, b, 1e-5), atol=3e-2,
+                               rtol=1e-2)
