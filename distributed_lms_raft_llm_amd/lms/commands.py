@@ -1,0 +1,73 @@
+"""The Raft log command format.
+
+Every log entry is ``{"term": int, "command": str}`` and ``command`` is
+``json.dumps({"operation": <op>, "args": [...]})`` -- exactly what the reference's live
+``create_log_entry`` emits (``lms_server.py:335-340``).  The six reference operations keep their
+names and argument orders:
+
+=====================  ==============================================  =======================
+operation              args (order)                                    proposed at (reference)
+=====================  ==============================================  =======================
+Register               [username, password, role]                      lms_server.py:749
+PostAssignment         [student, filename, file_path, assignment_text] lms_server.py:921
+PostCourseMaterial     [instructor, filename, file_path]               lms_server.py:902
+AskQuery               [username, query]                               lms_server.py:932
+RespondToQuery         [instructor, student_id, response]              lms_server.py:1017
+GradeAssignment        [student, grade]                                lms_server.py:1191
+=====================  ==============================================  =======================
+
+Additional operations of this implementation (new ``operation`` values, format unchanged):
+``NoOp`` (leader's first entry of a term), ``Login`` [username, token, role] / ``Logout``
+[token] (sessions survive leader failover), ``StoreBlob`` [filename, sha256, base64] (uploads
+replicate with the log) and ``SetVal`` [key, value] (the RaftService debug KV API).
+
+``decode`` also accepts the reference's shadowed legacy encoder (``lms_server.py:317-333``):
+``Op arg1 "multi word arg" ...`` (shlex quoting).
+"""
+from __future__ import annotations
+
+import json
+import shlex
+
+REFERENCE_OPS = {
+    "Register": 3,
+    "PostAssignment": 4,
+    "PostCourseMaterial": 3,
+    "AskQuery": 2,
+    "RespondToQuery": 3,
+    "GradeAssignment": 2,
+}
+EXTRA_OPS = {"NoOp": 0, "Login": 3, "Logout": 1, "StoreBlob": 3, "SetVal": 2}
+ALL_OPS = {**REFERENCE_OPS, **EXTRA_OPS}
+
+
+class BadCommand(ValueError):
+    pass
+
+
+def encode(operation: str, args: list) -> str:
+    if operation not in ALL_OPS:
+        raise BadCommand(f"unknown operation {operation!r}")
+    if len(args) != ALL_OPS[operation]:
+        raise BadCommand(f"{operation} takes {ALL_OPS[operation]} args, got {len(args)}")
+    return json.dumps({"operation": operation, "args": list(args)})
+
+
+def decode(command: str) -> tuple[str, list]:
+    s = command.strip()
+    if s.startswith("{"):
+        try:
+            obj = json.loads(s)
+        except ValueError as e:
+            raise BadCommand(f"malformed JSON command: {e}") from e
+        op, args = obj.get("operation"), obj.get("args", [])
+        if not isinstance(op, str) or not isinstance(args, list):
+            raise BadCommand("command must carry a string 'operation' and a list 'args'")
+        return op, args
+    try:
+        parts = shlex.split(s)
+    except ValueError as e:
+        raise BadCommand(f"malformed legacy command: {e}") from e
+    if not parts:
+        raise BadCommand("empty command")
+    return parts[0], parts[1:]

@@ -1,0 +1,143 @@
+"""LMS server process: Raft node + LMS/RaftService/FileTransferService on one gRPC port.
+
+CLI-compatible with the reference (``lms_server.py:1604-1613``)::
+
+    python lms_server.py <id> <port> <peer_address> [<peer_address> ...]
+
+The peers are the OTHER servers' addresses listed in server-id order, so with ids 1..N server
+``id`` maps peer position k to id ``k+1`` if ``k+1 < id`` else ``k+2`` -- the real ids (the
+reference keyed them 1..N-1 positionally, so server k never contacted server k+1, Appendix A.3).
+Everything else (data dir, tutoring address, relevance gate, timeouts) is an optional flag.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import threading
+from concurrent import futures
+
+import grpc
+
+from .. import wire
+from ..raft.core import RaftConfig
+from ..raft.node import RaftNode
+from ..raft.storage import FileStorage
+from ..raft.transport import GrpcTransport, RaftServicer, snapshot_handler
+from .service import FileTransferServicer, LMSServicer, TutoringClient
+from .state import LMSState
+
+log = logging.getLogger("dlms.server")
+
+
+def peer_ids(self_id: int, n_peers: int) -> list[int]:
+    return [i for i in range(1, n_peers + 2) if i != self_id]
+
+
+class LMSServer:
+    def __init__(self, node_id: int, port: int, peers: dict[int, str], data_dir: str, host: str = "[::]",
+                 advertise: str | None = None, tutor_address: str | None = None, gate=None,
+                 raft_config: RaftConfig | None = None, fsync: bool = True, workers: int = 32,
+                 snapshot_every: int = 2000):
+        self.id = node_id
+        self.port = port
+        self.peers = dict(peers)
+        self.address = advertise or f"localhost:{port}"
+        self.addresses = {**self.peers, node_id: self.address}
+        self.data_dir = data_dir
+        os.makedirs(data_dir, exist_ok=True)
+        self.storage = FileStorage(os.path.join(data_dir, "raft"), fsync=fsync)
+        self.state = LMSState(data_dir)
+        cfg = raft_config or RaftConfig()
+        self.transport = GrpcTransport(node_id, self.peers, rpc_timeout=max(cfg.rpc_timeout, 0.2))
+        self.node = RaftNode(node_id, self.peers, self.storage, self.state, self.transport, cfg,
+                             snapshot_every=snapshot_every)
+        self.transport.attach(self.node)
+        self.tutor = TutoringClient(tutor_address) if tutor_address else None
+        self.lms = LMSServicer(self.node, self.state, self.addresses, tutor=self.tutor, gate=gate)
+        if gate is not None and hasattr(gate, "attach_state"):
+            gate.attach_state(self.state)
+        opts = [("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
+                ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)]
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers), options=opts)
+        self.raft_servicer = RaftServicer(self.node, self.addresses, blocked=self.transport.blocked)
+        wire.register(self.server, "LMS", self.lms)
+        wire.register(self.server, "RaftService", self.raft_servicer)
+        wire.register(self.server, "FileTransferService", FileTransferServicer(self.state))
+        self.server.add_generic_rpc_handlers((snapshot_handler(self.node),))
+        bound = self.server.add_insecure_port(f"{host}:{port}")
+        if bound == 0:
+            raise RuntimeError(f"could not bind {host}:{port}")
+        self.port = bound
+
+    def start(self):
+        self.server.start()
+        self.node.start()
+        log.info("LMS server %d listening on %s (peers %s)", self.id, self.port, self.peers)
+        return self
+
+    def stop(self, grace: float = 0.5):
+        self.node.stop()
+        self.transport.close()
+        self.server.stop(grace).wait()
+        self.storage.close()
+        if self.tutor is not None:
+            self.tutor.close()
+
+    def isolate(self, peers: set[int]):
+        """Fault injection: drop all Raft traffic to/from ``peers`` (both directions)."""
+        self.transport.blocked.clear()
+        self.transport.blocked.update(peers)
+
+
+def build_arg_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="Raft-replicated LMS server (MI355X-native framework)")
+    ap.add_argument("id", type=int, help="this server's id (1..N)")
+    ap.add_argument("port", type=int)
+    ap.add_argument("peers", nargs="*", help="addresses of the other servers, in server-id order")
+    ap.add_argument("--host", default="[::]")
+    ap.add_argument("--advertise", default=None, help="address other nodes/clients use for this server")
+    ap.add_argument("--data-dir", default=None, help="default: ./lms_node<id>")
+    ap.add_argument("--tutor", default=os.environ.get("DLMS_TUTOR_ADDR", "localhost:50054"),
+                    help="tutoring server address ('' to disable)")
+    ap.add_argument("--gate", choices=["bert", "off"], default=os.environ.get("DLMS_GATE", "bert"))
+    ap.add_argument("--gate-model", default="bert-base-uncased")
+    ap.add_argument("--gate-device", default=os.environ.get("DLMS_GATE_DEVICE", "auto"))
+    ap.add_argument("--gate-threshold", type=float, default=0.6)
+    ap.add_argument("--gate-weights", default=None, help="local safetensors for the gate model")
+    ap.add_argument("--vocab", default=None, help="BERT vocab.txt (WordPiece); synthetic vocab if absent")
+    ap.add_argument("--election-timeout", default="0.15,0.30")
+    ap.add_argument("--heartbeat", type=float, default=0.05)
+    ap.add_argument("--no-fsync", action="store_true")
+    ap.add_argument("--snapshot-every", type=int, default=2000)
+    ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
+    return ap
+
+
+def main(argv=None):
+    args = build_arg_parser().parse_args(argv)
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    ids = peer_ids(args.id, len(args.peers))
+    peers = dict(zip(ids, args.peers))
+    lo, hi = (float(x) for x in args.election_timeout.split(","))
+    cfg = RaftConfig(election_timeout=(lo, hi), heartbeat_interval=args.heartbeat)
+    gate = None
+    if args.gate == "bert":
+        from ..gate.relevance import RelevanceGate
+
+        gate = RelevanceGate.create(model=args.gate_model, device=args.gate_device, threshold=args.gate_threshold,
+                                    weights=args.gate_weights, vocab=args.vocab)
+    srv = LMSServer(args.id, args.port, peers, args.data_dir or f"lms_node{args.id}", host=args.host,
+                    advertise=args.advertise, tutor_address=args.tutor or None, gate=gate, raft_config=cfg,
+                    fsync=not args.no_fsync, snapshot_every=args.snapshot_every).start()
+    done = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *a: done.set())
+    signal.signal(signal.SIGINT, lambda *a: done.set())
+    done.wait()
+    srv.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,364 @@
+"""``lms.LMS`` gRPC service: authentication, course workflows and the LLM tutoring path.
+
+Behaviour and every user-visible string follow the reference handlers
+(``lms_server.py:740-1274``) because ``lms_gui_final.py`` branches on them
+(e.g. ``"Grade not yet assigned"`` at ``lms_gui_final.py:790``).  What changes:
+
+* writes are proposed through Raft and the RPC returns after the entry is committed AND applied
+  (the reference acknowledges before replication); the reply strings stay the same;
+* a follower forwards any call to the current leader (the reference's follower writes crashed
+  with ``KeyError``, Appendix A.7) -- the GUI always asks ``WhoIsLeader`` first, so this only
+  matters during failover;
+* reads are served after a leader read-barrier, so an acknowledged write is always visible;
+* ``LMS.WhoIsLeader`` is implemented (the reference left it UNIMPLEMENTED, Appendix A.8);
+* ``GetLLMAnswer`` runs the BERT relevance gate with cached assignment embeddings and calls the
+  tutoring service with a deadline.
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import logging
+import time
+import uuid
+
+import grpc
+
+from .. import wire
+from ..raft.core import NotLeader
+from ..utils.metrics import METRICS
+from ..wire import pb
+from . import commands
+from .pdf import extract_text
+
+log = logging.getLogger("dlms.lms")
+
+FORWARD_HEADER = "x-dlms-forwarded"
+
+MSG_REGISTER_OK = "Registration request is being processed. Please wait."
+MSG_USER_EXISTS = "Username already exists."
+MSG_GRADE_OK = "Grading request is being processed. Please wait."
+MSG_BAD_TOKEN = "Invalid session token"
+MSG_ONLY_INSTRUCTORS_GRADE = "Only instructors can grade assignments"
+MSG_NO_STUDENT_ASSIGNMENT = "Student assignment not found"
+MSG_NO_MATERIALS = "No course materials available."
+MSG_BAD_GET = "Invalid request type or unauthorized access"
+MSG_INVALID_SESSION = "Invalid session"
+MSG_ONLY_STUDENTS_GRADES = "Only students can view grades"
+MSG_GRADE_NOT_ASSIGNED = "Grade not yet assigned"
+MSG_NO_GRADE = "No grade assigned yet."
+MSG_NO_ASSIGNMENTS = "No assignments found for this student."
+MSG_LLM_INVALID_SESSION = "Invalid session."
+MSG_LLM_ONLY_STUDENTS = "Only students can ask queries."
+MSG_LLM_NO_ASSIGNMENT = "No assignment found for this student."
+MSG_LLM_IRRELEVANT = ("Your query does not relate to your assignment. "
+                      "Please ask a question related to your assignment.")
+MSG_UNAVAILABLE = "The LMS cluster is unavailable (no leader). Please retry."
+MSG_TUTOR_UNAVAILABLE = "The tutoring service is unavailable. Please retry later."
+
+
+class TutoringClient:
+    def __init__(self, address: str, timeout: float = 120.0):
+        self.address = address
+        self.timeout = timeout
+        self._channel = wire.channel(address)
+        self._stub = wire.Stub("Tutoring", self._channel)
+
+    def ask(self, token: str, query: str) -> pb.QueryResponse:
+        return self._stub.GetLLMAnswer(pb.QueryRequest(token=token, query=query), timeout=self.timeout)
+
+    def close(self):
+        self._channel.close()
+
+
+class LMSServicer:
+    def __init__(self, node, state, addresses: dict[int, str], tutor: TutoringClient | None = None, gate=None,
+                 write_timeout: float = 5.0, forward_timeout: float = 130.0):
+        self.node = node
+        self.state = state
+        self.addresses = addresses
+        self.tutor = tutor
+        self.gate = gate
+        self.write_timeout = write_timeout
+        self.forward_timeout = forward_timeout
+        self._leader_stubs: dict[int, wire.Stub] = {}
+
+    # ------------------------------------------------------------------ plumbing
+    def _forward(self, method: str, request, context):
+        """If this node is not the leader, relay the call to the leader.  Returns the leader's
+        response, or None when the call should be served here."""
+        if self.node.is_leader:
+            return None
+        md = dict(context.invocation_metadata() or ())
+        if md.get(FORWARD_HEADER):
+            return None
+        lid = self.node.leader_id
+        if lid is None or lid not in self.addresses:
+            return None
+        stub = self._leader_stubs.get(lid)
+        if stub is None:
+            stub = wire.Stub("LMS", wire.channel(self.addresses[lid]))
+            self._leader_stubs[lid] = stub
+        try:
+            METRICS.inc("lms_forwarded_total")
+            return getattr(stub, method)(request, timeout=self.forward_timeout, metadata=((FORWARD_HEADER, "1"),))
+        except grpc.RpcError as e:
+            log.warning("forward %s to leader %s failed: %s", method, lid, e.code())
+            return None
+
+    def _write(self, op: str, args: list):
+        return self.node.propose(commands.encode(op, args), timeout=self.write_timeout)
+
+    def _write_many(self, items: list[tuple[str, list]]):
+        futs = [self.node.submit(commands.encode(op, a)) for op, a in items]
+        return [f.result(timeout=self.write_timeout) for f in futs]
+
+    def _read_fence(self):
+        if self.node.is_leader:
+            self.node.read_barrier(self.write_timeout)
+
+    def _session(self, token: str):
+        return self.state.session(token)
+
+    # ------------------------------------------------------------------ auth
+    def Register(self, request, context):
+        fwd = self._forward("Register", request, context)
+        if fwd is not None:
+            return fwd
+        self._read_fence()
+        if request.username in self.state.view()["users"]:
+            return pb.RegisterResponse(success=False, message=MSG_USER_EXISTS)
+        try:
+            ok = self._write("Register", [request.username, request.password, request.role])
+        except (NotLeader, TimeoutError, Exception):
+            return pb.RegisterResponse(success=False, message=MSG_UNAVAILABLE)
+        if not ok:
+            return pb.RegisterResponse(success=False, message=MSG_USER_EXISTS)
+        return pb.RegisterResponse(success=True, message=MSG_REGISTER_OK)
+
+    def Login(self, request, context):
+        fwd = self._forward("Login", request, context)
+        if fwd is not None:
+            return fwd
+        self._read_fence()
+        user = self.state.view()["users"].get(request.username)
+        if user is None or user["password"] != request.password:
+            return pb.LoginResponse(success=False)
+        token = str(uuid.uuid4())
+        try:
+            self._write("Login", [request.username, token, user["role"]])
+        except Exception:
+            return pb.LoginResponse(success=False)
+        return pb.LoginResponse(success=True, token=token, role=user["role"])
+
+    def Logout(self, request, context):
+        fwd = self._forward("Logout", request, context)
+        if fwd is not None:
+            return fwd
+        if self._session(request.token) is None:
+            return pb.LogoutResponse(success=False)
+        try:
+            ok = self._write("Logout", [request.token])
+        except Exception:
+            return pb.LogoutResponse(success=False)
+        return pb.LogoutResponse(success=bool(ok))
+
+    # ------------------------------------------------------------------ course workflows
+    def Post(self, request, context):
+        fwd = self._forward("Post", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None:
+            return pb.PostResponse(success=False)
+        user, role = s["username"], s["role"]
+        try:
+            if role == "instructor" and request.type == "course_material":
+                blob = bytes(request.file)
+                path = self.state.blobs.relpath(request.filename)
+                self._write_many([
+                    ("StoreBlob", [request.filename, hashlib.sha256(blob).hexdigest(), base64.b64encode(blob).decode()]),
+                    ("PostCourseMaterial", [user, request.filename, path]),
+                ])
+                return pb.PostResponse(success=True)
+            if role == "student" and request.type == "assignment":
+                blob = bytes(request.file)
+                text = extract_text(blob)
+                path = self.state.blobs.relpath(request.filename)
+                self._write_many([
+                    ("StoreBlob", [request.filename, hashlib.sha256(blob).hexdigest(), base64.b64encode(blob).decode()]),
+                    ("PostAssignment", [user, request.filename, path, text]),
+                ])
+                return pb.PostResponse(success=True)
+            if role == "student" and request.type == "query":
+                self._write("AskQuery", [user, request.data])
+                return pb.PostResponse(success=True)
+        except Exception as e:
+            log.warning("Post failed: %s", e)
+        return pb.PostResponse(success=False)
+
+    def Get(self, request, context):
+        fwd = self._forward("Get", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None:
+            return pb.GetResponse(success=False)
+        self._read_fence()
+        data = self.state.view()
+        if request.type == "course_material" and s["role"] == "student":
+            mats = data["course_materials"]
+            if not mats:
+                return pb.GetResponse(success=True, message=MSG_NO_MATERIALS)
+            return pb.GetResponse(success=True, entries=[
+                pb.DataEntry(id="1", filename=m["filename"], file=self.state.blobs.get(m["filepath"]),
+                             instructor=m.get("instructor", "Unknown")) for m in mats])
+        if s["role"] == "instructor" and request.type == "student_list":
+            entries = []
+            for student, items in data["assignments"].items():
+                for a in items:
+                    entries.append(pb.DataEntry(id=student, filename=a["filename"],
+                                                file=self.state.blobs.get(a["filepath"])))
+            return pb.GetResponse(success=True, entries=entries)
+        return pb.GetResponse(success=False, message=MSG_BAD_GET)
+
+    def GradeAssignment(self, request, context):
+        fwd = self._forward("GradeAssignment", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None:
+            return pb.GradeResponse(success=False, message=MSG_BAD_TOKEN)
+        if s["role"] != "instructor":
+            return pb.GradeResponse(success=False, message=MSG_ONLY_INSTRUCTORS_GRADE)
+        self._read_fence()
+        if request.studentId not in self.state.view()["assignments"]:
+            return pb.GradeResponse(success=False, message=MSG_NO_STUDENT_ASSIGNMENT)
+        try:
+            self._write("GradeAssignment", [request.studentId, request.grade])
+        except Exception:
+            return pb.GradeResponse(success=False, message=MSG_UNAVAILABLE)
+        return pb.GradeResponse(success=True, message=MSG_GRADE_OK)
+
+    def GetGrade(self, request, context):
+        fwd = self._forward("GetGrade", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None:
+            return pb.GetGradeResponse(success=False, grade=MSG_INVALID_SESSION)
+        if s["role"] != "student":
+            return pb.GetGradeResponse(success=False, grade=MSG_ONLY_STUDENTS_GRADES)
+        self._read_fence()
+        items = self.state.view()["assignments"].get(s["username"])
+        if items is None:
+            return pb.GetGradeResponse(success=True, grade=MSG_NO_ASSIGNMENTS)
+        for a in items:
+            if "grade" in a:
+                if a["grade"] is None:
+                    return pb.GetGradeResponse(success=True, grade=MSG_GRADE_NOT_ASSIGNED)
+                return pb.GetGradeResponse(success=True, grade=f"Your grade: {a['grade']}")
+        return pb.GetGradeResponse(success=True, grade=MSG_NO_GRADE)
+
+    # ------------------------------------------------------------------ queries
+    def GetUnansweredQueries(self, request, context):
+        fwd = self._forward("GetUnansweredQueries", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None or s["role"] != "instructor":
+            return pb.GetResponse(success=False)
+        self._read_fence()
+        entries = []
+        for student, qs in self.state.view().get("queries", {}).items():
+            for q in qs:
+                if "query" in q and "response" in q and not q["answered"]:
+                    entries.append(pb.DataEntry(id=student, data=q["query"]))
+        return pb.GetResponse(success=True, entries=entries)
+
+    def RespondToQuery(self, request, context):
+        fwd = self._forward("RespondToQuery", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None or s["role"] != "instructor":
+            return pb.PostResponse(success=False)
+        try:
+            self._write("RespondToQuery", [s["username"], request.studentId, request.data])
+        except Exception:
+            return pb.PostResponse(success=False)
+        return pb.PostResponse(success=True)
+
+    def GetInstructorResponse(self, request, context):
+        fwd = self._forward("GetInstructorResponse", request, context)
+        if fwd is not None:
+            return fwd
+        s = self._session(request.token)
+        if s is None or s["role"] != "student":
+            return pb.GetResponse(success=False)
+        self._read_fence()
+        user = s["username"]
+        entries = [pb.DataEntry(id=user, data=f"Your Query: {q['query']}\nInstructor Response: {q['response']}")
+                   for q in self.state.view().get("queries", {}).get(user, []) if q.get("answered", False)]
+        return pb.GetResponse(success=True, entries=entries)
+
+    # ------------------------------------------------------------------ LLM tutoring
+    def GetLLMAnswer(self, request, context):
+        t0 = time.perf_counter()
+        s = self._session(request.token)
+        if s is None:
+            # sessions replicate through the log; a brand-new token may not have reached this node yet
+            fwd = self._forward("GetLLMAnswer", request, context)
+            if fwd is not None:
+                return fwd
+            return pb.QueryResponse(success=True, response=MSG_LLM_INVALID_SESSION)
+        if s["role"] != "student":
+            return pb.QueryResponse(success=True, response=MSG_LLM_ONLY_STUDENTS)
+        items = self.state.view()["assignments"].get(s["username"])
+        if not items:
+            return pb.QueryResponse(success=True, response=MSG_LLM_NO_ASSIGNMENT)
+        assignment_text = items[0]["text"]
+        if self.gate is not None:
+            tg = time.perf_counter()
+            relevant, sim = self.gate.check(request.query, assignment_text)
+            METRICS.observe("gate_ms", (time.perf_counter() - tg) * 1e3)
+            METRICS.observe("gate_similarity", sim)
+            if not relevant:
+                METRICS.inc("gate_rejected_total")
+                return pb.QueryResponse(success=True, response=MSG_LLM_IRRELEVANT)
+        if self.tutor is None:
+            return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        try:
+            resp = self.tutor.ask(request.token, request.query)
+        except grpc.RpcError as e:
+            log.warning("tutoring call failed: %s", e.code())
+            return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        METRICS.observe("llm_answer_ms", (time.perf_counter() - t0) * 1e3)
+        return resp
+
+    def WhoIsLeader(self, request, context):
+        lid = self.node.leader_id
+        return pb.LeaderResponse(leader_id=lid if lid is not None else -1)
+
+
+class FileTransferServicer:
+    """``lms.FileTransferService.SendFile``: a reference server can still stream an upload to us.
+    Writes land under ``uploads/`` only (the client-supplied path is reduced to its basename),
+    atomically and idempotently -- the reference appended (``'ab'``), duplicating bytes on retry."""
+
+    def __init__(self, state):
+        self.state = state
+
+    def SendFile(self, request_iterator, context):
+        name, buf = None, bytearray()
+        try:
+            for chunk in request_iterator:
+                if name is None:
+                    name = chunk.destination_path
+                buf += chunk.content
+            if name is None:
+                return pb.FileTransferResponse(status="Error receiving file: empty stream")
+            self.state.blobs.put(name, bytes(buf))
+            return pb.FileTransferResponse(status="File received successfully")
+        except Exception as e:  # mirror the reference's error reporting
+            return pb.FileTransferResponse(status=f"Error receiving file: {e}")

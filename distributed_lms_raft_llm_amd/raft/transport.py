@@ -1,0 +1,177 @@
+"""gRPC transport for Raft: the control plane stays on the reference's ``RaftService`` RPCs.
+
+Core messages map onto ``lms.proto``:
+
+==================  ================================================================================
+VoteRequest         RequestVoteRequest{candidate: TermCandIDPair{term, candidateID}, lastLogIndex,
+                    lastLogTerm}
+VoteResponse        RequestVoteResponse{result: TermResultPair{term, verdict}}
+AppendRequest       AppendEntriesRequest{leader: TermLeaderIDPair{leaderID, term}, prevLogIndex,
+                    prevLogTerm, entries: [LogEntry{term, command}], leaderCommit}
+AppendResponse      AppendEntriesResponse{result: {term, verdict}, success, term}: ``result.term`` is
+                    the responder's current term; the spare ``term`` field (the reference never
+                    fills it) carries the match index on success / the back-off hint on failure
+==================  ================================================================================
+
+InstallSnapshot has no RPC in ``lms.proto`` (which stays byte-for-byte), so it is served on an
+internal generic method ``/lmsinternal.Raft/InstallSnapshot`` with a JSON body.
+
+Differences from the reference's call pattern (``lms_server.py:442-650``): one persistent channel
+per peer instead of a new channel per RPC, deadlines on every RPC, and sends happen on a per-peer
+single-thread executor so a slow peer never blocks the node or the other peers.
+"""
+from __future__ import annotations
+
+import json
+import logging
+from concurrent.futures import ThreadPoolExecutor
+
+import grpc
+
+from .. import wire
+from ..wire import pb
+from .core import (AppendRequest, AppendResponse, Entry, SnapshotRequest, SnapshotResponse, VoteRequest,
+                   VoteResponse)
+
+log = logging.getLogger("dlms.raft.transport")
+
+SNAPSHOT_METHOD = "/lmsinternal.Raft/InstallSnapshot"
+
+
+def to_proto(m):
+    if isinstance(m, VoteRequest):
+        return pb.RequestVoteRequest(candidate=pb.TermCandIDPair(term=m.term, candidateID=m.src),
+                                     lastLogIndex=m.last_log_index, lastLogTerm=m.last_log_term)
+    if isinstance(m, VoteResponse):
+        return pb.RequestVoteResponse(result=pb.TermResultPair(term=m.term, verdict=m.granted))
+    if isinstance(m, AppendRequest):
+        return pb.AppendEntriesRequest(leader=pb.TermLeaderIDPair(leaderID=m.src, term=m.term),
+                                       prevLogIndex=m.prev_index, prevLogTerm=m.prev_term,
+                                       entries=[pb.LogEntry(term=e.term, command=e.command) for e in m.entries],
+                                       leaderCommit=m.leader_commit)
+    if isinstance(m, AppendResponse):
+        return pb.AppendEntriesResponse(result=pb.TermResultPair(term=m.term, verdict=m.success), term=m.index,
+                                        success=m.success)
+    raise TypeError(type(m))
+
+
+def vote_request_from(p, dst: int) -> VoteRequest:
+    return VoteRequest(p.candidate.candidateID, dst, p.candidate.term, p.lastLogIndex, p.lastLogTerm)
+
+
+def append_request_from(p, dst: int) -> AppendRequest:
+    return AppendRequest(p.leader.leaderID, dst, p.leader.term, p.prevLogIndex, p.prevLogTerm,
+                         [Entry(e.term, e.command) for e in p.entries], p.leaderCommit)
+
+
+class GrpcTransport:
+    def __init__(self, self_id: int, peers: dict[int, str], rpc_timeout: float = 0.5,
+                 snapshot_timeout: float = 30.0):
+        self.id = self_id
+        self.node = None
+        self.rpc_timeout = rpc_timeout
+        self.snapshot_timeout = snapshot_timeout
+        self._channels = {pid: wire.channel(addr) for pid, addr in peers.items()}
+        self._stubs = {pid: wire.Stub("RaftService", ch) for pid, ch in self._channels.items()}
+        self._snap = {pid: ch.unary_unary(SNAPSHOT_METHOD) for pid, ch in self._channels.items()}
+        self._pools = {pid: ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"raft-send-{pid}")
+                       for pid in peers}
+        self.blocked: set[int] = set()  # fault injection: peers we pretend not to reach
+        self.closed = False
+
+    def attach(self, node):
+        self.node = node
+
+    def send(self, m):
+        if self.closed or m.dst not in self._pools or m.dst in self.blocked:
+            return
+        self._pools[m.dst].submit(self._send_sync, m)
+
+    def _send_sync(self, m):
+        try:
+            if isinstance(m, VoteRequest):
+                r = self._stubs[m.dst].RequestVote(to_proto(m), timeout=self.rpc_timeout)
+                resp = VoteResponse(m.dst, self.id, r.result.term, r.result.verdict)
+            elif isinstance(m, AppendRequest):
+                r = self._stubs[m.dst].AppendEntries(to_proto(m), timeout=self.rpc_timeout)
+                resp = AppendResponse(m.dst, self.id, r.result.term, r.result.verdict, r.term)
+            elif isinstance(m, SnapshotRequest):
+                body = json.dumps({"src": m.src, "term": m.term, "last_index": m.last_index,
+                                   "last_term": m.last_term, "data": m.data}).encode()
+                r = json.loads(self._snap[m.dst](body, timeout=self.snapshot_timeout))
+                resp = SnapshotResponse(m.dst, self.id, r["term"], r["last_index"])
+            else:
+                return
+        except grpc.RpcError:
+            return  # the core's in-flight timeout retries
+        except Exception:
+            log.exception("raft send to %s failed", m.dst)
+            return
+        if self.node is not None and not self.closed and m.dst not in self.blocked:
+            self.node.deliver(resp)
+
+    def close(self):
+        self.closed = True
+        for p in self._pools.values():
+            p.shutdown(wait=False, cancel_futures=True)
+        for ch in self._channels.values():
+            ch.close()
+
+
+class RaftServicer:
+    """Server side of ``lms.RaftService`` (registered through ``wire.register``)."""
+
+    def __init__(self, node, address_of=None, blocked=None):
+        self.node = node
+        self.address_of = address_of or {}
+        self.blocked = blocked if blocked is not None else set()
+
+    def _check(self, src, context):
+        if src in self.blocked:
+            context.abort(grpc.StatusCode.UNAVAILABLE, "partitioned (fault injection)")
+
+    def RequestVote(self, request, context):
+        self._check(request.candidate.candidateID, context)
+        r = self.node.handle(vote_request_from(request, self.node.id))
+        return to_proto(r)
+
+    def AppendEntries(self, request, context):
+        self._check(request.leader.leaderID, context)
+        r = self.node.handle(append_request_from(request, self.node.id))
+        return to_proto(r)
+
+    def WhoIsLeader(self, request, context):
+        lid = self.node.leader_id
+        return pb.LeaderResponse(leader_id=lid if lid is not None else -1)
+
+    def GetLeader(self, request, context):
+        lid = self.node.leader_id
+        if lid is None:
+            return pb.GetLeaderResponse(nodeId=-1, nodeAddress="")
+        return pb.GetLeaderResponse(nodeId=lid, nodeAddress=self.address_of.get(lid, ""))
+
+    def SetVal(self, request, context):
+        from ..lms import commands
+
+        try:
+            self.node.propose(commands.encode("SetVal", [request.key, request.value]))
+            return pb.SetValResponse(verdict=True)
+        except Exception:
+            return pb.SetValResponse(verdict=False)
+
+    def GetVal(self, request, context):
+        kv = getattr(self.node.sm, "kv", {})
+        if request.key in kv:
+            return pb.GetValResponse(verdict=True, value=kv[request.key])
+        return pb.GetValResponse(verdict=False, value="")
+
+
+def snapshot_handler(node):
+    def install(body: bytes, context) -> bytes:
+        obj = json.loads(body)
+        r = node.handle(SnapshotRequest(obj["src"], node.id, obj["term"], obj["last_index"], obj["last_term"],
+                                        obj["data"]))
+        return json.dumps({"term": r.term, "last_index": r.last_index}).encode()
+
+    return grpc.method_handlers_generic_handler("lmsinternal.Raft", {
+        "InstallSnapshot": grpc.unary_unary_rpc_method_handler(install)})

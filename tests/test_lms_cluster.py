@@ -1,0 +1,142 @@
+"""LMS service over a real 3-node Raft cluster on localhost: the authorization matrix and exact
+strings of SURVEY.md §2.5, commit-before-ack, replicated sessions and uploads, failover."""
+import time
+
+import pytest
+
+from distributed_lms_raft_llm_amd.lms import service as S
+from distributed_lms_raft_llm_amd.lms.pdf import make_pdf
+from distributed_lms_raft_llm_amd.wire import pb
+from lms_harness import Cluster, KeywordGate, start_tutor
+
+pytestmark = pytest.mark.timeout(120)
+
+
+@pytest.fixture
+def cluster(tmp_path):
+    tsrv, tport, tutor = start_tutor()
+    c = Cluster(3, tmp_path, tutor_address=f"127.0.0.1:{tport}", gate=KeywordGate())
+    c.tutor = tutor
+    yield c
+    c.close()
+    tsrv.stop(0)
+
+
+def login(stub, user, pw="pw"):
+    r = stub.Login(pb.LoginRequest(username=user, password=pw), timeout=10)
+    assert r.success
+    return r.token
+
+
+def test_full_workflow_exact_strings(cluster):
+    lid = cluster.wait_leader()
+    st = cluster.stub(lid)
+    r = st.Register(pb.RegisterRequest(username="alice", password="pw", role="student"), timeout=10)
+    assert r.success and r.message == S.MSG_REGISTER_OK
+    r = st.Register(pb.RegisterRequest(username="alice", password="x", role="student"), timeout=10)
+    assert not r.success and r.message == S.MSG_USER_EXISTS
+    st.Register(pb.RegisterRequest(username="bob", password="pw", role="instructor"), timeout=10)
+    assert not st.Login(pb.LoginRequest(username="alice", password="wrong"), timeout=10).success
+    ta, tb = login(st, "alice"), login(st, "bob")
+    assert st.Login(pb.LoginRequest(username="alice", password="pw"), timeout=10).role == "student"
+
+    # course materials
+    g = st.Get(pb.GetRequest(token=ta, type="course_material"), timeout=10)
+    assert g.success and g.message == S.MSG_NO_MATERIALS and len(g.entries) == 0
+    assert not st.Post(pb.PostRequest(token=ta, type="course_material", file=b"x", filename="m.pdf"),
+                       timeout=10).success
+    assert st.Post(pb.PostRequest(token=tb, type="course_material", file=b"slides", filename="m.pdf"),
+                   timeout=10).success
+    g = st.Get(pb.GetRequest(token=ta, type="course_material"), timeout=10)
+    assert [(e.id, e.filename, e.file, e.instructor) for e in g.entries] == [("1", "m.pdf", b"slides", "bob")]
+    g = st.Get(pb.GetRequest(token=tb, type="course_material"), timeout=10)
+    assert not g.success and g.message == S.MSG_BAD_GET
+
+    # grades before any assignment
+    assert st.GetGrade(pb.GetGradeRequest(token=ta), timeout=10).grade == S.MSG_NO_ASSIGNMENTS
+    r = st.GradeAssignment(pb.GradeRequest(token=tb, studentId="alice", grade="A"), timeout=10)
+    assert not r.success and r.message == S.MSG_NO_STUDENT_ASSIGNMENT
+    # assignment upload (a real PDF: text is extracted into the log entry)
+    pdf = make_pdf("Raft log replication and leader election")
+    assert st.Post(pb.PostRequest(token=ta, type="assignment", file=pdf, filename="hw1.pdf"), timeout=10).success
+    assert st.GetGrade(pb.GetGradeRequest(token=ta), timeout=10).grade == S.MSG_GRADE_NOT_ASSIGNED
+    g = st.Get(pb.GetRequest(token=tb, type="student_list"), timeout=10)
+    assert [(e.id, e.filename, e.file) for e in g.entries] == [("alice", "hw1.pdf", pdf)]
+    r = st.GradeAssignment(pb.GradeRequest(token=ta, studentId="alice", grade="A"), timeout=10)
+    assert not r.success and r.message == S.MSG_ONLY_INSTRUCTORS_GRADE
+    r = st.GradeAssignment(pb.GradeRequest(token="nope", studentId="alice", grade="A"), timeout=10)
+    assert not r.success and r.message == S.MSG_BAD_TOKEN
+    r = st.GradeAssignment(pb.GradeRequest(token=tb, studentId="alice", grade="A"), timeout=10)
+    assert r.success and r.message == S.MSG_GRADE_OK
+    assert st.GetGrade(pb.GetGradeRequest(token=ta), timeout=10).grade == "Your grade: A"
+    r = st.GetGrade(pb.GetGradeRequest(token=tb), timeout=10)
+    assert not r.success and r.grade == S.MSG_ONLY_STUDENTS_GRADES
+    r = st.GetGrade(pb.GetGradeRequest(token="bad"), timeout=10)
+    assert not r.success and r.grade == S.MSG_INVALID_SESSION
+
+    # instructor queries
+    assert st.Post(pb.PostRequest(token=ta, type="query", data="when is the exam?"), timeout=10).success
+    u = st.GetUnansweredQueries(pb.GetRequest(token=tb), timeout=10)
+    assert [(e.id, e.data) for e in u.entries] == [("alice", "when is the exam?")]
+    assert not st.GetUnansweredQueries(pb.GetRequest(token=ta), timeout=10).success
+    assert st.RespondToQuery(pb.PostRequest(token=tb, studentId="alice", data="Friday"), timeout=10).success
+    assert len(st.GetUnansweredQueries(pb.GetRequest(token=tb), timeout=10).entries) == 0
+    resp = st.GetInstructorResponse(pb.GetRequest(token=ta), timeout=10)
+    assert [e.data for e in resp.entries] == ["Your Query: when is the exam?\nInstructor Response: Friday"]
+
+    # LLM path: gate + tutoring
+    r = st.GetLLMAnswer(pb.QueryRequest(token=ta, query="explain leader election"), timeout=30)
+    assert r.success and r.response.startswith("Question: explain leader election")
+    r = st.GetLLMAnswer(pb.QueryRequest(token=ta, query="best pizza toppings"), timeout=30)
+    assert r.success and r.response == S.MSG_LLM_IRRELEVANT
+    assert st.GetLLMAnswer(pb.QueryRequest(token=tb, query="x"), timeout=30).response == S.MSG_LLM_ONLY_STUDENTS
+    assert st.GetLLMAnswer(pb.QueryRequest(token="bad", query="x"), timeout=30).response == S.MSG_LLM_INVALID_SESSION
+    assert cluster.tutor.calls == ["explain leader election"]
+
+    assert st.Logout(pb.LogoutRequest(token=ta), timeout=10).success
+    assert not st.Logout(pb.LogoutRequest(token=ta), timeout=10).success
+
+
+def test_state_replicated_to_followers_and_lms_whoisleader(cluster):
+    lid = cluster.wait_leader()
+    st = cluster.stub(lid)
+    st.Register(pb.RegisterRequest(username="carol", password="pw", role="student"), timeout=10)
+    tok = login(st, "carol")
+    st.Post(pb.PostRequest(token=tok, type="assignment", file=b"plain text homework", filename="a.txt"), timeout=10)
+    time.sleep(0.5)
+    for i, srv in cluster.servers.items():
+        d = srv.state.view()
+        assert "carol" in d["users"]
+        assert d["assignments"]["carol"][0]["text"] == "plain text homework"
+        assert srv.state.blobs.get("uploads/a.txt") == b"plain text homework"
+        assert srv.state.session(tok) is not None
+        assert cluster.stub(i).WhoIsLeader(pb.Empty(), timeout=5).leader_id == lid
+
+
+def test_follower_forwards_writes(cluster):
+    lid = cluster.wait_leader()
+    f = [i for i in cluster.servers if i != lid][0]
+    st = cluster.stub(f)
+    r = st.Register(pb.RegisterRequest(username="dave", password="pw", role="student"), timeout=10)
+    assert r.success and r.message == S.MSG_REGISTER_OK
+    assert login(st, "dave")
+
+
+def test_leader_failover_keeps_data_and_sessions(cluster):
+    lid = cluster.wait_leader()
+    st = cluster.stub(lid)
+    st.Register(pb.RegisterRequest(username="erin", password="pw", role="student"), timeout=10)
+    tok = login(st, "erin")
+    st.Post(pb.PostRequest(token=tok, type="query", data="q1"), timeout=10)
+    t0 = time.time()
+    cluster.stop(lid)
+    new = cluster.wait_leader(timeout=10)
+    elapsed = time.time() - t0
+    assert new != lid
+    assert elapsed < 3.0, elapsed  # reference: ~102 s
+    st2 = cluster.stub(new)
+    # the session created on the old leader is still valid (replicated Login entry)
+    assert st2.Post(pb.PostRequest(token=tok, type="query", data="q2"), timeout=10).success
+    assert st2.GetGrade(pb.GetGradeRequest(token=tok), timeout=10).grade == S.MSG_NO_ASSIGNMENTS
+    d = cluster.servers[new].state.view()
+    assert [q["query"] for q in d["queries"]["erin"]] == ["q1", "q2"]
