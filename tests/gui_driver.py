@@ -1,0 +1,112 @@
+"""Runs the reference ``lms_gui_final.py`` UNCHANGED (fake headless tkinter, address-rewrite shim
+for its hard-coded 172.18.18.x server list) against a live cluster and scripts a session the way
+its button lambdas do.  Prints the dialog log and observations as one JSON line.
+
+usage: python gui_driver.py <reference_dir> <addr_map_json> <workdir>
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def main():
+    ref_dir, addr_map, workdir = sys.argv[1], json.loads(sys.argv[2]), sys.argv[3]
+    sys.path.insert(0, os.path.join(HERE, "fake_tk"))
+    sys.path.insert(0, ref_dir)
+    import grpc
+
+    real = grpc.insecure_channel
+
+    def shim(target, *a, **k):
+        return real(addr_map.get(target, target), *a, **k)
+
+    grpc.insecure_channel = shim
+    import tkinter as tk
+    from tkinter import filedialog, messagebox
+
+    import lms_gui_final as gui
+
+    out = {"steps": []}
+
+    def click(text, idx=-1):
+        bs = tk.find_buttons(text)
+        assert bs, f"no button {text!r}"
+        bs[idx].invoke()
+
+    def dialogs_after(n, timeout=60):
+        log = messagebox.wait_for(n + 1, timeout)
+        return log[n] if len(log) > n else None
+
+    root = tk.Tk()
+    app = gui.LMSApp(root)
+    out["leader_address"] = app.leader_address
+
+    def register(user, role):
+        n = len(messagebox.LOG)
+        click("Register")  # login screen -> register screen
+        app.reg_username.insert(0, user)
+        app.reg_password.insert(0, "pw")
+        app.reg_role.set(role)
+        click("Register")  # submit on the register screen
+        out["steps"].append(["register", user, dialogs_after(n)])
+
+    def login(user):
+        app.username.insert(0, user)
+        app.password.insert(0, "pw")
+        click("Login")
+        end = time.time() + 30
+        while app.token is None and time.time() < end:
+            time.sleep(0.02)
+        out["steps"].append(["login", user, app.role])
+
+    def logout():
+        n = len(messagebox.LOG)
+        click("Logout")
+        out["steps"].append(["logout", dialogs_after(n)])
+
+    register("stud", "student")
+    register("prof", "instructor")
+    login("stud")
+    # post assignment through the file-path entry
+    path = os.path.join(workdir, "homework.pdf")
+    from distributed_lms_raft_llm_amd.lms.pdf import make_pdf
+
+    with open(path, "wb") as f:
+        f.write(make_pdf("Raft consensus: leader election and log replication"))
+    n = len(messagebox.LOG)
+    click("Post Assignment")
+    app.file_path.insert(0, path)
+    click("Submit")
+    out["steps"].append(["post_assignment", dialogs_after(n)])
+    n = len(messagebox.LOG)
+    click("Go Back")
+    click("View Grades")
+    out["steps"].append(["view_grades", dialogs_after(n)])
+    # LLM query (radio default "llm")
+    n = len(messagebox.LOG)
+    click("Ask Query")
+    app.query_text.insert(0, "how does raft leader election work")
+    click("Submit Query")
+    out["steps"].append(["ask_llm", dialogs_after(n)])
+    # instructor question
+    n = len(messagebox.LOG)
+    click("Go Back")
+    click("Ask Query")
+    app.query_text.insert(0, "office hours?")
+    app.query_option.set("instructor")
+    click("Submit Query")
+    out["steps"].append(["ask_instructor", dialogs_after(n)])
+    click("Go Back")
+    logout()
+    login("prof")
+    out["steps"].append(["instructor_menu", bool(tk.find_buttons("View and Grade Assignments"))])
+    logout()
+    print("GUI_RESULT " + json.dumps(out), flush=True)
+    os._exit(0)  # the GUI's executor threads are non-daemon
+
+
+if __name__ == "__main__":
+    main()
