@@ -1,0 +1,84 @@
+"""BERT relevance-gate encoder on MI355X (K13-K17): packed variable-length batches, no padding.
+
+Per layer (post-LN BERT):
+    QKV GEMM (one [3H, H] weight; q out, k/v scattered per sequence) -> bidirectional attention
+    -> out-proj (fp32 partials) -> fused residual-add + LayerNorm (eps 1e-12, f32 + bf16 outputs)
+    -> intermediate GEMM with fused bias + exact-erf GELU -> output GEMM (partials)
+    -> fused residual-add + LayerNorm
+then the mean-pool kernel over each sequence's rows and the batched cosine kernel.
+Embedding gather + LayerNorm is one fused kernel.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..models.config import BertConfig
+
+
+class HipBertEncoder:
+    def __init__(self, cfg: BertConfig, weights: dict[str, torch.Tensor], device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HipBertEncoder needs a GPU")
+        ops.lib()
+        self.cfg = cfg
+        self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
+        dev, f32, bf = self.device, torch.float32, torch.bfloat16
+
+        def t(name, dt=f32):
+            return weights[name].to(device=dev, dtype=dt).contiguous()
+
+        self.word = t("embeddings.word_embeddings.weight")
+        self.pos = t("embeddings.position_embeddings.weight")
+        self.type0 = t("embeddings.token_type_embeddings.weight")[0].contiguous()
+        self.emb_g, self.emb_b = t("embeddings.LayerNorm.weight"), t("embeddings.LayerNorm.bias")
+        self.layers = []
+        for i in range(cfg.n_layer):
+            p = f"encoder.layer.{i}."
+            wqkv = torch.cat([weights[p + f"attention.self.{n}.weight"] for n in ("query", "key", "value")], 0)
+            bqkv = torch.cat([weights[p + f"attention.self.{n}.bias"] for n in ("query", "key", "value")], 0)
+            self.layers.append(dict(
+                w_qkv=wqkv.to(dev, bf).contiguous(), b_qkv=bqkv.to(dev, f32).contiguous(),
+                w_o=t(p + "attention.output.dense.weight", bf), b_o=t(p + "attention.output.dense.bias"),
+                ln1_g=t(p + "attention.output.LayerNorm.weight"), ln1_b=t(p + "attention.output.LayerNorm.bias"),
+                w_i=t(p + "intermediate.dense.weight", bf), b_i=t(p + "intermediate.dense.bias"),
+                w_out=t(p + "output.dense.weight", bf), b_out=t(p + "output.dense.bias"),
+                ln2_g=t(p + "output.LayerNorm.weight"), ln2_b=t(p + "output.LayerNorm.bias"),
+            ))
+
+    @torch.no_grad()
+    def embed(self, batch: list[list[int]]) -> torch.Tensor:
+        """Mean-pooled last hidden state per sequence: f32 [len(batch), H]."""
+        cfg, dev = self.cfg, self.device
+        lens = [min(len(ids), cfg.max_position) for ids in batch]
+        R, n, S = sum(lens), len(batch), max(lens)
+        H, nh, eps = cfg.hidden, cfg.n_head, cfg.layer_norm_eps
+        ids = torch.tensor([i for b, L in zip(batch, lens) for i in b[:L]], dtype=torch.int32).to(dev, non_blocking=True)
+        pos = torch.tensor([j for L in lens for j in range(L)], dtype=torch.int32).to(dev, non_blocking=True)
+        seq = torch.tensor([b for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32).to(dev, non_blocking=True)
+        kvlen = torch.tensor([L for L in lens for _ in range(L)], dtype=torch.int32).to(dev, non_blocking=True)
+        starts = torch.tensor([sum(lens[:b]) for b in range(n)], dtype=torch.int32).to(dev, non_blocking=True)
+        lens_d = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
+        x, h = ops.bert_embed_ln(ids, pos, self.word, self.pos, self.type0, self.emb_g, self.emb_b, eps)
+        bf = torch.bfloat16
+        q = torch.empty(R, H, dtype=bf, device=dev)
+        att = torch.empty(R, H, dtype=bf, device=dev)
+        ff = torch.empty(R, cfg.intermediate, dtype=bf, device=dev)
+        kc = torch.empty(n, nh, S, 64, dtype=bf, device=dev)
+        vc = torch.empty_like(kc)
+        parts = torch.empty(1, R, H, dtype=torch.float32, device=dev)
+        for lw in self.layers:
+            ops.gemm(h, lw["w_qkv"], ops.EPI_QKV, bias=lw["b_qkv"], q_out=q, k_cache=kc, v_cache=vc, row_slot=seq,
+                     row_pos=pos)
+            ops.row_attention(q, kc, vc, seq, kvlen, out=att)
+            ops.gemm(att, lw["w_o"], ops.EPI_PARTIAL, out=parts, split_k=1)
+            ops.add_layernorm(x, lw["ln1_g"], lw["ln1_b"], eps, parts=parts, nsplit=1, bias=lw["b_o"], out_bf16=h,
+                              store_normed=True)
+            ops.gemm(h, lw["w_i"], ops.EPI_GELU_ERF, bias=lw["b_i"], out=ff)
+            ops.gemm(ff, lw["w_out"], ops.EPI_PARTIAL, out=parts, split_k=1)
+            ops.add_layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, parts=parts, nsplit=1, bias=lw["b_out"], out_bf16=h,
+                              store_normed=True)
+        return ops.mean_pool(x, starts, lens_d)
+
+    def cosine(self, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+        return ops.cosine(a.contiguous(), b.contiguous())

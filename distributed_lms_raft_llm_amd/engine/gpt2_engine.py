@@ -58,6 +58,22 @@ def seen_bitmap(tokens, words: int) -> np.ndarray:
     return bm.view(np.int32)
 
 
+def passthrough(prompts, T: int, eos: int):
+    """``generate()`` semantics for degenerate prompts: one already at/over ``max_length`` comes
+    back unchanged (nothing is generated); an empty prompt starts from EOS (GPT-2's BOS).
+    Returns (results with pass-through entries filled, indices of prompts that must run,
+    normalised copies of all prompts)."""
+    norm = [list(p) if len(p) else [eos] for p in prompts]
+    out: list = [None] * len(prompts)
+    run = []
+    for i, p in enumerate(norm):
+        if len(p) >= T:
+            out[i] = p
+        else:
+            run.append(i)
+    return out, run, norm
+
+
 def _bucket(n: int) -> int:
     for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024):
         if n <= b:
@@ -304,12 +320,18 @@ class HipGPT2Engine:
         n = len(prompts)
         if n == 0:
             return []
+        done, run_idx, prompts = passthrough(prompts, T, self.cfg.eos_token_id)
+        if len(run_idx) < n:
+            sub = self.generate([prompts[i] for i in run_idx], max_length, repetition_penalty, stats) if run_idx else []
+            for i, o in zip(run_idx, sub):
+                done[i] = o
+            return done
         if n > self.max_batch:
             out: list[list[int]] = []
             for i in range(0, n, self.max_batch):
                 out += self.generate(prompts[i: i + self.max_batch], max_length, repetition_penalty, stats)
             return out
-        prompts = [list(p)[-T:] if len(p) else [self.cfg.eos_token_id] for p in prompts]
+        prompts = [list(p) for p in prompts]
         B = min(_bucket(n), self.max_batch)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -363,12 +385,17 @@ class TorchGPT2Engine:
         from ..models.gpt2 import reference_generate
 
         T = self.max_length if max_length is None else max_length
-        prompts = [list(p)[-T:] if len(p) else [self.cfg.eos_token_id] for p in prompts]
+        out, run_idx, norm = passthrough(prompts, T, self.cfg.eos_token_id)
+        prompts = [norm[i] for i in run_idx]
         t0 = time.perf_counter()
-        out = reference_generate(self.model, prompts, max_length=T, repetition_penalty=repetition_penalty)
+        if prompts:
+            gen = reference_generate(self.model, prompts, max_length=T, repetition_penalty=repetition_penalty)
+            for i, o in zip(run_idx, gen):
+                out[i] = o
+        out_run = [out[i] for i in run_idx]
         if stats is not None:
             stats.batch += len(prompts)
             stats.prompt_tokens += sum(map(len, prompts))
-            stats.new_tokens += sum(len(o) - len(p) for o, p in zip(out, prompts))
+            stats.new_tokens += sum(len(o) - len(p) for o, p in zip(out_run, prompts))
             stats.decode_ms += (time.perf_counter() - t0) * 1e3
         return out

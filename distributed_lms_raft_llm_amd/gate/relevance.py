@@ -1,0 +1,106 @@
+"""BERT relevance gate for ``GetLLMAnswer`` (C11, ``lms_server.py:97-104,1249-1271``).
+
+Semantics kept: bert-base-uncased, mean of ``last_hidden_state`` over all tokens ([CLS] and [SEP]
+included), truncation at 512 tokens, cosine similarity, reject when ``< 0.6``.
+
+What changes (SURVEY.md §7.1 design choice 2): the model is built ONCE per process (the reference
+re-loads it from disk on every query, ~563 ms), runs on the MI355X through the HIP kernels
+(``engine/bert_engine.py``) -- or the torch reference on CPU hosts -- and assignment embeddings are
+computed when the PostAssignment entry is applied and cached, so a query costs one short
+encoder pass.
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import threading
+from collections import OrderedDict
+
+import torch
+
+from ..models.bert import BertReference, init_bert_weights, load_bert_safetensors
+from ..models.config import bert_config
+from ..tokenizer import BertWordPiece
+
+log = logging.getLogger("dlms.gate")
+
+
+class RelevanceGate:
+    def __init__(self, encoder, tokenizer: BertWordPiece, threshold: float = 0.6, cache_size: int = 4096):
+        self.encoder = encoder
+        self.tok = tokenizer
+        self.threshold = threshold
+        self._cache: OrderedDict[str, torch.Tensor] = OrderedDict()
+        self._cache_size = cache_size
+        self._lock = threading.Lock()  # one encoder pass at a time (GPU stream / CPU threads)
+        self.device = getattr(encoder, "device", torch.device("cpu"))
+
+    @classmethod
+    def create(cls, model: str = "bert-base-uncased", device: str = "auto", threshold: float = 0.6,
+               weights: str | None = None, vocab: str | None = None, seed: int = 0):
+        cfg = bert_config(model)
+        w = load_bert_safetensors(weights) if weights else init_bert_weights(cfg, seed=seed)
+        if device == "auto":
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if str(device).startswith("cuda"):
+            from ..engine.bert_engine import HipBertEncoder
+
+            enc = HipBertEncoder(cfg, w, device=device)
+        else:
+            enc = BertReference(cfg, w, device="cpu")
+        tok = BertWordPiece(vocab, vocab_size=cfg.vocab_size, max_length=cfg.max_position)
+        log.info("relevance gate: %s on %s (%s vocab)", model, device, "synthetic" if tok.synthetic else "real")
+        return cls(enc, tok, threshold)
+
+    # ------------------------------------------------------------------ embeddings
+    @staticmethod
+    def _key(text: str) -> str:
+        return hashlib.sha1(text.encode("utf-8")).hexdigest()
+
+    def embed(self, texts: list[str]) -> torch.Tensor:
+        ids = [self.tok.encode(t) for t in texts]
+        with self._lock, torch.no_grad():
+            return self.encoder.embed(ids).float()
+
+    def _cached(self, text: str) -> torch.Tensor:
+        k = self._key(text)
+        with self._lock:
+            v = self._cache.get(k)
+            if v is not None:
+                self._cache.move_to_end(k)
+                return v
+        v = self.embed([text])[0]
+        with self._lock:
+            self._cache[k] = v
+            if len(self._cache) > self._cache_size:
+                self._cache.popitem(last=False)
+        return v
+
+    def warm(self, text: str):
+        self._cached(text)
+
+    def similarity(self, query: str, text: str) -> float:
+        q = self.embed([query])[0]
+        a = self._cached(text)
+        if hasattr(self.encoder, "cosine"):
+            return float(self.encoder.cosine(q[None], a[None])[0, 0])
+        return float(torch.nn.functional.cosine_similarity(q[None], a[None]).item())
+
+    def check(self, query: str, assignment_text: str) -> tuple[bool, float]:
+        s = self.similarity(query, assignment_text)
+        return s >= self.threshold, s
+
+    def attach_state(self, state):
+        """Embed assignment texts as PostAssignment entries are applied (off the query path)."""
+
+        def on_apply(op, args):
+            if op == "PostAssignment" and len(args) == 4:
+                threading.Thread(target=self._safe_warm, args=(args[3],), daemon=True).start()
+
+        state.listeners.append(on_apply)
+
+    def _safe_warm(self, text):
+        try:
+            self.warm(text)
+        except Exception:
+            log.exception("gate warm-up failed")

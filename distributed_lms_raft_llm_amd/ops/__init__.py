@@ -85,7 +85,7 @@ def _bind(L):
         "dlms_gemm": [I, P, I, P, I, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_layernorm": [P, I, P, P, P, I, P, I, I, I, F, P],
         "dlms_layernorm_gather": [P, I, P, P, P, P, I, I, I, F, P],
-        "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, I, I, F, P],
+        "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, I, I, F, I, P],
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
         "dlms_decode_update": [P, I, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I, I, P],
@@ -252,8 +252,10 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
 
 
 def add_layernorm(x: torch.Tensor, gamma, beta, eps: float, *, parts: torch.Tensor | None = None, nsplit: int = 0,
-                  bias: torch.Tensor | None = None, out_bf16: torch.Tensor | None = None, want_out: bool = True):
-    """x += bias + sum(parts[:nsplit]) (in place), then out = bf16(LN(x)).  parts: f32 [S, >=M, >=D]."""
+                  bias: torch.Tensor | None = None, out_bf16: torch.Tensor | None = None, want_out: bool = True,
+                  store_normed: bool = False):
+    """v = x + bias + sum(parts[:nsplit]); x <- v (or LN(v) when ``store_normed``: post-LN models);
+    out = bf16(LN(v)).  parts: f32 [S, >=M, >=D]."""
     _req(x, torch.float32, "x", 2)
     M, D = x.shape
     if D % 4 or D > 2048 or gamma.numel() != D or beta.numel() != D:
@@ -276,7 +278,8 @@ def add_layernorm(x: torch.Tensor, gamma, beta, eps: float, *, parts: torch.Tens
             raise ValueError("add_layernorm: out too small")
     _check(lib().dlms_add_layernorm(_p(x), x.stride(0), _p(parts) if nsplit else None, ldp, sstride, nsplit,
                                     _p(bias), _p(gamma), _p(beta), _p(out_bf16),
-                                    out_bf16.stride(0) if out_bf16 is not None else 0, M, D, float(eps), _stream()),
+                                    out_bf16.stride(0) if out_bf16 is not None else 0, M, D, float(eps),
+                                    int(store_normed), _stream()),
            "dlms_add_layernorm")
     return out_bf16
 

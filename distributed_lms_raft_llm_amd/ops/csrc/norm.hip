@@ -123,7 +123,8 @@ extern "C" hipError_t dlms_layernorm_gather(const float* x, int ldx, const int* 
 // Fused residual update + LayerNorm (one wave per row, 64-thread workgroups so a decode batch of
 // B rows spreads over B CUs):
 //     v = x + bias + sum_{s < nsplit} parts[s]      (fixed summation order: deterministic)
-//     x = v            (when anything was added)
+//     x = v            (when anything was added; pre-LN GPT-2 residual stream)
+//     x = LN(v)        (instead, when store_normed: post-LN BERT residual stream)
 //     out = bf16(LN(v) * gamma + beta)               (skipped when out == nullptr)
 // This consumes the split-K partial slabs of the previous projection GEMM (EPI_PARTIAL) or, under
 // tensor parallelism, the all-reduced partial, so no GEMM epilogue ever read-modify-writes x.
@@ -133,13 +134,13 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* x, int ldx, co
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, bf16_t* out, int ldb,
-                                                           int M, int D, float eps) {
+                                                           int M, int D, float eps, int store_normed) {
     const int lane = threadIdx.x;
     const int row = blockIdx.x;
     if (row >= M) return;
     const int nv = D >> 2;
     float4* xr = reinterpret_cast<float4*>(x + (size_t)row * ldx);
-    const bool update = NSPLIT > 0 || bias != nullptr;
+    const bool update = (NSPLIT > 0 || bias != nullptr) && !store_normed;
     float4 v[LN_MAX_V4];
     float s = 0.f;
 #pragma unroll
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* x, int ldx, co
         }
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
-    if (out == nullptr) return;
+    if (out == nullptr && !store_normed) return;
     const float mean = wave_sum(s) / (float)D;
     float ss = 0.f;
 #pragma unroll
@@ -185,20 +186,26 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* x, int ldx, co
             uint2 p;
             p.x = pack_bf16x2((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y);
             p.y = pack_bf16x2((v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
-            reinterpret_cast<uint2*>(out + (size_t)row * ldb)[c] = p;
+            if (out) reinterpret_cast<uint2*>(out + (size_t)row * ldb)[c] = p;
+            if (store_normed) {  // post-LN residual stream (BERT): x <- LN(x + ...)
+                const float4 y = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
+                                             (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+                xr[c] = y;
+            }
         }
     }
 }
 
 extern "C" hipError_t dlms_add_layernorm(float* x, int ldx, const float* parts, int ldp, long long split_stride,
                                          int nsplit, const float* bias, const float* gamma, const float* beta,
-                                         void* out_bf16, int ldb, int M, int D, float eps, hipStream_t stream) {
+                                         void* out_bf16, int ldb, int M, int D, float eps, int store_normed,
+                                         hipStream_t stream) {
     if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0 || nsplit < 0 || nsplit > 8) return hipErrorInvalidValue;
     bf16_t* o = reinterpret_cast<bf16_t*>(out_bf16);
 #define ADD_LN_CASE(NS)                                                                                       \
     case NS:                                                                                                  \
         hipLaunchKernelGGL(add_layernorm_kernel<NS>, dim3(M), dim3(64), 0, stream, x, ldx, parts, ldp, split_stride, \
-                           bias, gamma, beta, o, ldb, M, D, eps);                                             \
+                           bias, gamma, beta, o, ldb, M, D, eps, store_normed);                                             \
         break;
     switch (nsplit) {
         ADD_LN_CASE(0) ADD_LN_CASE(1) ADD_LN_CASE(2) ADD_LN_CASE(3) ADD_LN_CASE(4) ADD_LN_CASE(5) ADD_LN_CASE(6)

@@ -1,0 +1,201 @@
+"""Tutoring service (``lms.Tutoring.GetLLMAnswer``) backed by the MI355X GPT-2 engine.
+
+Reference behaviour (``tutoring_server.py:15-49``): wrap the query in a fixed prompt, run GPT-2
+``generate(max_length=150, repetition_penalty=1.2)`` (greedy), return the decoded sequence -- prompt
+included -- with ``success=True``; listen on ``[::]:50054`` with 10 worker threads.
+
+Here concurrent queries are batched: a batcher thread collects requests for up to
+``batch_window_ms`` (or until ``max_batch``) and runs them as ONE batched prefill + hipGraph decode
+on the GPU (``engine/gpt2_engine.py``); on a CPU-only host the same batching runs on the torch
+reference engine (BASELINE config 1).  Per-request latency, batch sizes and tokens/s land in the
+metrics registry.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import queue
+import signal
+import threading
+import time
+from concurrent import futures
+from dataclasses import dataclass
+
+import grpc
+import torch
+
+from .. import wire
+from ..models.config import GenerationConfig, gpt2_config
+from ..models.gpt2 import init_gpt2_weights, load_safetensors_weights
+from ..tokenizer import GPT2BPE
+from ..utils.metrics import METRICS
+from ..wire import pb
+
+log = logging.getLogger("dlms.tutor")
+
+PROMPT_TEMPLATE = ("You are an intelligent assistant. Answer the following question in detail:\n"
+                   "Question: {query}\nAnswer:")
+
+
+def build_prompt(query: str) -> str:
+    return PROMPT_TEMPLATE.format(query=query)
+
+
+@dataclass
+class _Req:
+    ids: list[int]
+    fut: futures.Future
+    t0: float
+
+
+class Batcher:
+    """Dynamic batching in front of an engine with ``generate(prompts, max_length, penalty)``."""
+
+    def __init__(self, engine, gen: GenerationConfig, max_batch: int = 64, window_ms: float = 2.0):
+        self.engine = engine
+        self.gen = gen
+        self.max_batch = max_batch
+        self.window = window_ms / 1e3
+        self.q: queue.Queue = queue.Queue()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._loop, name="tutor-batcher", daemon=True)
+        self._t.start()
+
+    def submit(self, ids: list[int]) -> futures.Future:
+        f: futures.Future = futures.Future()
+        self.q.put(_Req(ids, f, time.perf_counter()))
+        METRICS.set("tutor_queue_depth", self.q.qsize())
+        return f
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                first = self.q.get(timeout=0.1)
+            except queue.Empty:
+                continue
+            batch = [first]
+            deadline = time.perf_counter() + self.window
+            while len(batch) < self.max_batch:
+                rem = deadline - time.perf_counter()
+                if rem <= 0:
+                    break
+                try:
+                    batch.append(self.q.get(timeout=rem))
+                except queue.Empty:
+                    break
+            self._run(batch)
+
+    def _run(self, batch: list[_Req]):
+        t0 = time.perf_counter()
+        try:
+            outs = self.engine.generate([r.ids for r in batch], self.gen.max_length, self.gen.repetition_penalty)
+        except Exception as e:  # fail the whole batch, keep serving
+            log.exception("generation failed")
+            for r in batch:
+                r.fut.set_exception(e)
+            return
+        dt = time.perf_counter() - t0
+        new = sum(len(o) - len(r.ids) for o, r in zip(outs, batch))
+        METRICS.observe("tutor_batch_size", len(batch))
+        METRICS.observe("tutor_batch_ms", dt * 1e3)
+        METRICS.inc("tutor_tokens_generated", new)
+        METRICS.set("tutor_tokens_per_s", new / dt if dt > 0 else 0.0)
+        now = time.perf_counter()
+        for o, r in zip(outs, batch):
+            METRICS.observe("tutor_query_ms", (now - r.t0) * 1e3)
+            r.fut.set_result(o)
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(timeout=2)
+
+
+class TutoringServicer:
+    def __init__(self, batcher: Batcher, tokenizer: GPT2BPE, max_length: int, timeout: float = 300.0):
+        self.batcher = batcher
+        self.tok = tokenizer
+        self.max_length = max_length
+        self.timeout = timeout
+
+    def GetLLMAnswer(self, request, context):
+        # like generate(), a prompt already at max_length comes back unchanged (engines handle it)
+        ids = self.tok.encode(build_prompt(request.query))
+        try:
+            out = self.batcher.submit(ids).result(timeout=self.timeout)
+        except Exception as e:
+            context.abort(grpc.StatusCode.INTERNAL, f"generation failed: {e}")
+        return pb.QueryResponse(success=True, response=self.tok.decode(out, skip_special_tokens=True))
+
+
+def make_engine(model: str, device: str, max_batch: int, max_length: int, weights: str | None = None, seed: int = 0,
+                tp_group=None):
+    cfg = gpt2_config(model)
+    w = load_safetensors_weights(weights) if weights else init_gpt2_weights(cfg, seed=seed)
+    if device == "auto":
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    if device.startswith("cuda"):
+        from ..engine.gpt2_engine import HipGPT2Engine
+
+        return HipGPT2Engine(cfg, w, device=device, max_batch=max_batch, max_length=max_length, tp_group=tp_group)
+    from ..engine.gpt2_engine import TorchGPT2Engine
+
+    return TorchGPT2Engine(cfg, w, max_length=max_length)
+
+
+class TutoringServer:
+    def __init__(self, engine, port: int = 50054, host: str = "[::]", max_batch: int = 64, window_ms: float = 2.0,
+                 max_length: int = 150, repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None,
+                 workers: int = 64):
+        self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
+        self.tok = tokenizer or GPT2BPE(eos_token_id=getattr(getattr(engine, "cfg", None), "eos_token_id", 50256))
+        self.batcher = Batcher(engine, self.gen, max_batch=max_batch, window_ms=window_ms)
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
+                                  options=[("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
+                                           ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)])
+        wire.register(self.server, "Tutoring", TutoringServicer(self.batcher, self.tok, max_length))
+        self.port = self.server.add_insecure_port(f"{host}:{port}")
+        if self.port == 0:
+            raise RuntimeError(f"could not bind {host}:{port}")
+
+    def start(self):
+        self.server.start()
+        log.info("tutoring server on port %d", self.port)
+        return self
+
+    def stop(self):
+        self.server.stop(0.5).wait()
+        self.batcher.stop()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="GPT-2 tutoring server (MI355X HIP engine)")
+    ap.add_argument("--port", type=int, default=int(os.environ.get("DLMS_TUTOR_PORT", "50054")))
+    ap.add_argument("--host", default="[::]")
+    ap.add_argument("--model", default=os.environ.get("DLMS_MODEL", "gpt2"))
+    ap.add_argument("--weights", default=None, help="local safetensors checkpoint (HF GPT-2 layout)")
+    ap.add_argument("--vocab", default=None, help="GPT-2 vocab.json")
+    ap.add_argument("--merges", default=None, help="GPT-2 merges.txt")
+    ap.add_argument("--device", default=os.environ.get("DLMS_DEVICE", "auto"))
+    ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--window-ms", type=float, default=2.0)
+    ap.add_argument("--max-length", type=int, default=150)
+    ap.add_argument("--repetition-penalty", type=float, default=1.2)
+    ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
+    args = ap.parse_args(argv)
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights)
+    tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
+    srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
+                         args.repetition_penalty, tokenizer=tok).start()
+    print(f"Tutoring Server started on port {srv.port}", flush=True)
+    done = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *a: done.set())
+    signal.signal(signal.SIGINT, lambda *a: done.set())
+    done.wait()
+    srv.stop()
+
+
+if __name__ == "__main__":
+    main()
