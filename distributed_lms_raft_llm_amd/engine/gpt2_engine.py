@@ -152,7 +152,13 @@ class HipGPT2Engine:
             import torch.distributed as dist
 
             flat = self.all_keys.view(-1)[: self.tp_size * B]
-            dist.all_gather_into_tensor(flat, self.local_keys[:B], group=self.tp_group)
+            if dist.get_backend(self.tp_group) == "nccl":
+                dist.all_gather_into_tensor(flat, self.local_keys[:B], group=self.tp_group)
+            else:  # gloo (functional TP tests on one GPU): list all-gather, eager only
+                parts = list(flat.view(self.tp_size, B).unbind(0))
+                dist.all_gather(parts, self.local_keys[:B].clone(), group=self.tp_group)
+                for i, p in enumerate(parts):
+                    flat.view(self.tp_size, B)[i].copy_(p)
             return flat.view(self.tp_size, B)
         return self.local_keys[:B]
 

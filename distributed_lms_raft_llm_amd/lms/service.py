@@ -126,7 +126,7 @@ class LMSServicer:
         if fwd is not None:
             return fwd
         self._read_fence()
-        if request.username in self.state.view()["users"]:
+        if self.state.read(lambda d: request.username in d["users"]):
             return pb.RegisterResponse(success=False, message=MSG_USER_EXISTS)
         try:
             ok = self._write("Register", [request.username, request.password, request.role])
@@ -141,7 +141,7 @@ class LMSServicer:
         if fwd is not None:
             return fwd
         self._read_fence()
-        user = self.state.view()["users"].get(request.username)
+        user = self.state.read(lambda d: dict(d["users"][request.username]) if request.username in d["users"] else None)
         if user is None or user["password"] != request.password:
             return pb.LoginResponse(success=False)
         token = str(uuid.uuid4())
@@ -205,21 +205,18 @@ class LMSServicer:
         if s is None:
             return pb.GetResponse(success=False)
         self._read_fence()
-        data = self.state.view()
         if request.type == "course_material" and s["role"] == "student":
-            mats = data["course_materials"]
+            mats = self.state.read(lambda d: [(m["filename"], m["filepath"], m.get("instructor", "Unknown"))
+                                              for m in d["course_materials"]])
             if not mats:
                 return pb.GetResponse(success=True, message=MSG_NO_MATERIALS)
             return pb.GetResponse(success=True, entries=[
-                pb.DataEntry(id="1", filename=m["filename"], file=self.state.blobs.get(m["filepath"]),
-                             instructor=m.get("instructor", "Unknown")) for m in mats])
+                pb.DataEntry(id="1", filename=f, file=self.state.blobs.get(p), instructor=ins) for f, p, ins in mats])
         if s["role"] == "instructor" and request.type == "student_list":
-            entries = []
-            for student, items in data["assignments"].items():
-                for a in items:
-                    entries.append(pb.DataEntry(id=student, filename=a["filename"],
-                                                file=self.state.blobs.get(a["filepath"])))
-            return pb.GetResponse(success=True, entries=entries)
+            rows = self.state.read(lambda d: [(st, a["filename"], a["filepath"]) for st, items in d["assignments"].items()
+                                              for a in items])
+            return pb.GetResponse(success=True, entries=[
+                pb.DataEntry(id=st, filename=f, file=self.state.blobs.get(p)) for st, f, p in rows])
         return pb.GetResponse(success=False, message=MSG_BAD_GET)
 
     def GradeAssignment(self, request, context):
@@ -232,7 +229,7 @@ class LMSServicer:
         if s["role"] != "instructor":
             return pb.GradeResponse(success=False, message=MSG_ONLY_INSTRUCTORS_GRADE)
         self._read_fence()
-        if request.studentId not in self.state.view()["assignments"]:
+        if not self.state.read(lambda d: request.studentId in d["assignments"]):
             return pb.GradeResponse(success=False, message=MSG_NO_STUDENT_ASSIGNMENT)
         try:
             self._write("GradeAssignment", [request.studentId, request.grade])
@@ -250,7 +247,8 @@ class LMSServicer:
         if s["role"] != "student":
             return pb.GetGradeResponse(success=False, grade=MSG_ONLY_STUDENTS_GRADES)
         self._read_fence()
-        items = self.state.view()["assignments"].get(s["username"])
+        user = s["username"]
+        items = self.state.read(lambda d: [dict(a) for a in d["assignments"][user]] if user in d["assignments"] else None)
         if items is None:
             return pb.GetGradeResponse(success=True, grade=MSG_NO_ASSIGNMENTS)
         for a in items:
@@ -269,12 +267,9 @@ class LMSServicer:
         if s is None or s["role"] != "instructor":
             return pb.GetResponse(success=False)
         self._read_fence()
-        entries = []
-        for student, qs in self.state.view().get("queries", {}).items():
-            for q in qs:
-                if "query" in q and "response" in q and not q["answered"]:
-                    entries.append(pb.DataEntry(id=student, data=q["query"]))
-        return pb.GetResponse(success=True, entries=entries)
+        rows = self.state.read(lambda d: [(st, q["query"]) for st, qs in d.get("queries", {}).items() for q in qs
+                                          if "query" in q and "response" in q and not q["answered"]])
+        return pb.GetResponse(success=True, entries=[pb.DataEntry(id=st, data=q) for st, q in rows])
 
     def RespondToQuery(self, request, context):
         fwd = self._forward("RespondToQuery", request, context)
@@ -298,9 +293,9 @@ class LMSServicer:
             return pb.GetResponse(success=False)
         self._read_fence()
         user = s["username"]
-        entries = [pb.DataEntry(id=user, data=f"Your Query: {q['query']}\nInstructor Response: {q['response']}")
-                   for q in self.state.view().get("queries", {}).get(user, []) if q.get("answered", False)]
-        return pb.GetResponse(success=True, entries=entries)
+        texts = self.state.read(lambda d: [f"Your Query: {q['query']}\nInstructor Response: {q['response']}"
+                                           for q in d.get("queries", {}).get(user, []) if q.get("answered", False)])
+        return pb.GetResponse(success=True, entries=[pb.DataEntry(id=user, data=t) for t in texts])
 
     # ------------------------------------------------------------------ LLM tutoring
     def GetLLMAnswer(self, request, context):
@@ -314,10 +309,11 @@ class LMSServicer:
             return pb.QueryResponse(success=True, response=MSG_LLM_INVALID_SESSION)
         if s["role"] != "student":
             return pb.QueryResponse(success=True, response=MSG_LLM_ONLY_STUDENTS)
-        items = self.state.view()["assignments"].get(s["username"])
-        if not items:
+        user = s["username"]
+        assignment_text = self.state.read(
+            lambda d: d["assignments"][user][0]["text"] if d["assignments"].get(user) else None)
+        if assignment_text is None:
             return pb.QueryResponse(success=True, response=MSG_LLM_NO_ASSIGNMENT)
-        assignment_text = items[0]["text"]
         if self.gate is not None:
             tg = time.perf_counter()
             relevant, sim = self.gate.check(request.query, assignment_text)

@@ -245,6 +245,13 @@ class LMSState:
                 return None
             return {"username": s["username"], "role": user["role"]}
 
+    def read(self, fn):
+        """Run ``fn(data)`` under the state lock; ``fn`` must copy out what it returns.  The read
+        path of every RPC (no whole-state copies: state grows with every upload)."""
+        with self.lock:
+            return fn(self.data)
+
     def view(self) -> dict:
+        """Deep copy of the whole state (tests / debugging only)."""
         with self.lock:
             return copy.deepcopy(self.data)
