@@ -87,6 +87,7 @@ def _bind(L):
         "dlms_layernorm_gather": [P, I, P, P, P, P, I, I, I, F, P],
         "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, I, I, F, I, P],
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
+        "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
         "dlms_decode_update": [P, I, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I, I, P],
         "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
@@ -97,6 +98,8 @@ def _bind(L):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    L.dlms_gemm_force_tile.argtypes = [ctypes.c_int]
+    L.dlms_gemm_force_tile.restype = None
     L.dlms_error_string.argtypes = [ctypes.c_int]
     L.dlms_error_string.restype = ctypes.c_char_p
     L.dlms_gemm_epi_size.restype = ctypes.c_int
@@ -299,8 +302,11 @@ def layernorm_gather(x: torch.Tensor, rows: torch.Tensor, gamma, beta, eps: floa
 
 
 def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
-                  row_kvlen: torch.Tensor, out: torch.Tensor | None = None, scale: float | None = None):
-    """q: bf16 [R, H*64]; caches bf16 [slots, H, t_max, 64]; row r attends keys [0, row_kvlen[r])."""
+                  row_kvlen: torch.Tensor, out: torch.Tensor | None = None, scale: float | None = None,
+                  impl: str = "wave"):
+    """q: bf16 [R, H*64]; caches bf16 [slots, H, t_max, 64]; row r attends keys [0, row_kvlen[r]).
+    impl "wave": one wave per (row, head), online softmax (default); "lds": block per (row, head),
+    exact two-pass softmax through LDS (t_max <= 2048)."""
     _req(q, torch.bfloat16, "q", 2)
     _req(k_cache, torch.bfloat16, "k_cache", 4)
     _req(v_cache, torch.bfloat16, "v_cache", 4)
@@ -316,8 +322,9 @@ def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=q.device)
     _req(out, torch.bfloat16, "out", 2)
     sc = (1.0 / 8.0) if scale is None else scale
-    _check(lib().dlms_row_attention(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
-                                    _p(out), out.stride(0), R, H, T, float(sc), _stream()), "dlms_row_attention")
+    fn = lib().dlms_attention if impl == "wave" else lib().dlms_row_attention
+    _check(fn(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen), _p(out), out.stride(0), R, H,
+              T, float(sc), _stream()), "attention")
     return out
 
 

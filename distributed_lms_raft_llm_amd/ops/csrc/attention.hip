@@ -104,6 +104,108 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
     }
 }
 
+// Decode-shaped attention: ONE WAVE per (row, head), 4 heads of a row per workgroup (their cache
+// rows are adjacent).  Lane (g = lane>>3, c = lane&7) owns dims [8c, 8c+8) of keys t = 8i + g;
+// a wave-instruction therefore reads 8 whole 128-B key rows (1 KiB contiguous).  Online softmax
+// in registers (exp2 with log2(e) folded into q), ATT_UNROLL key-steps of K and V loads issued
+// before any use, then a shuffle merge of the 8 per-group (max, sum, acc) triples.  No LDS, no
+// barriers: the kernel is a pure KV stream.
+#define ATT_UNROLL 4
+
+__global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                        const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                                        const int* __restrict__ row_slot,
+                                                        const int* __restrict__ row_kvlen, bf16_t* out, int ldo, int H,
+                                                        int t_max, float scale_log2) {
+    const int lane = threadIdx.x & 63;
+    const int h = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int r = blockIdx.y;
+    if (h >= H) return;
+    const int g = lane >> 3;
+    const int c = lane & 7;
+    const int slot = row_slot[r];
+    int kvlen = row_kvlen[r];
+    kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
+    const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+    const bf16_t* K = kc + head_off + c * 8;
+    const bf16_t* V = vc + head_off + c * 8;
+
+    float qf[8];
+    unpack8(*reinterpret_cast<const uint4*>(q + (size_t)r * ldq + h * 64 + c * 8), qf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[j] *= scale_log2;
+
+    float m = -INFINITY, l = 0.f;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t0 = 0; t0 < kvlen; t0 += 8 * ATT_UNROLL) {
+        uint4 kr[ATT_UNROLL], vr[ATT_UNROLL];
+#pragma unroll
+        for (int u = 0; u < ATT_UNROLL; ++u) {
+            int t = t0 + u * 8 + g;
+            t = t < kvlen ? t : kvlen - 1;  // clamped (masked below): loads never leave the slot
+            kr[u] = *reinterpret_cast<const uint4*>(K + (size_t)t * 64);
+            vr[u] = *reinterpret_cast<const uint4*>(V + (size_t)t * 64);
+        }
+#pragma unroll
+        for (int u = 0; u < ATT_UNROLL; ++u) {
+            float kf[8];
+            unpack8(kr[u], kf);
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
+            s += __shfl_xor(s, 1, 64);
+            s += __shfl_xor(s, 2, 64);
+            s += __shfl_xor(s, 4, 64);
+            const bool valid = t0 + u * 8 + g < kvlen;
+            if (valid) {
+                const float m_new = fmaxf(m, s);
+                const float corr = exp2f(m - m_new);  // m == -inf -> 0 (acc and l are 0 then)
+                const float p = exp2f(s - m_new);
+                float vf[8];
+                unpack8(vr[u], vf);
+                l = l * corr + p;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] = acc[j] * corr + p * vf[j];
+                m = m_new;
+            }
+        }
+    }
+    // merge the 8 key groups (lanes c, c+8, ..., c+56 hold partials of the same dims)
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+        const float m_o = __shfl_xor(m, o, 64);
+        const float l_o = __shfl_xor(l, o, 64);
+        const float m_n = fmaxf(m, m_o);
+        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
+        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
+        l = l * a + l_o * b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x_o = __shfl_xor(acc[j], o, 64);
+            acc[j] = acc[j] * a + x_o * b;
+        }
+        m = m_n;
+    }
+    if (g == 0) {
+        const float inv = 1.f / l;
+        float o8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o8[j] = acc[j] * inv;
+        *reinterpret_cast<uint4*>(out + (size_t)r * ldo + h * 64 + c * 8) = pack8(o8);
+    }
+}
+
+extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
+                                     const int* row_kvlen, void* out, int ldo, int R, int H, int t_max, float scale,
+                                     hipStream_t stream) {
+    if (R <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
+    const float scale_log2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(attn_wave_kernel, dim3((H + 3) / 4, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q),
+                       ldq, reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
+                       row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale_log2);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t dlms_row_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                          const int* row_kvlen, void* out, int ldo, int R, int H, int t_max,
                                          float scale, hipStream_t stream) {

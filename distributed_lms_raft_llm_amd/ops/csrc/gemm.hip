@@ -266,10 +266,41 @@ static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int
 // Tile selection.  Decode GEMMs (M = live batch <= 256) are latency-bound: prefer the tile count
 // that covers the 256 CUs; prefill / encoder / LM-head GEMMs take 128-wide tiles (less operand
 // re-reading per MFMA).
+static int g_force_tile = -1;  // tuning override (dlms_gemm_force_tile), -1 = heuristic
+
+template <int EPI>
+static hipError_t launch_forced(int id, const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
+                                const GemmEpi& ep, hipStream_t stream, bool* done) {
+    *done = true;
+    switch (id) {
+        case 0: return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 1: return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 2: return launch_gemm_cfg<128, 64, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 4: return launch_gemm_cfg<64, 64, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 7: return launch_gemm_cfg<64, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        default: break;
+    }
+    if (N % 128 == 0) {
+        switch (id) {
+            case 3: return launch_gemm_cfg<128, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 5: return launch_gemm_cfg<64, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 6: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            default: break;
+        }
+    }
+    *done = false;
+    return hipSuccess;
+}
+
 template <int EPI>
 static hipError_t launch_gemm_epi(const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
     const int split = EPI == EPI_PARTIAL ? ep.split_k : 1;
+    if (g_force_tile >= 0) {
+        bool done = false;
+        hipError_t e = launch_forced<EPI>(g_force_tile, A, lda, W, ldw, M, N, K, ep, stream, &done);
+        if (done) return e;
+    }
     if (M <= 32) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     const long t128x128 = (long)((M + 127) / 128) * (N / 128) * split;
     const long t128x64 = (long)((M + 127) / 128) * (N / 64) * split;
@@ -277,6 +308,8 @@ static hipError_t launch_gemm_epi(const bf16_t* A, int lda, const bf16_t* W, int
     if (t128x64 >= 256) return launch_gemm_cfg<128, 64, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
 }
+
+extern "C" void dlms_gemm_force_tile(int id) { g_force_tile = id; }
 
 extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                 const GemmEpi* ep, hipStream_t stream) {

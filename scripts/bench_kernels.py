@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Per-kernel microbenchmark of the decode hot path (GPT-2 shapes) on one MI355X.
 
-Times every kernel shape the decode step launches, in one process with interleaved repetitions
-(cdna_hip_programming.md §5.4 rule 24), on random data, and prints a JSON summary with achieved
-TFLOP/s and GB/s (unique bytes) per shape.
+Each measurement captures ``--inner`` back-to-back launches of one kernel into a hipGraph and
+times graph replays with events (host launch overhead excluded, inter-kernel boundaries
+included -- what the decode graph pays), interleaving variants in one process
+(cdna_hip_programming.md §5.4 rule 24) on random data.  GEMM tiles can be forced to sweep the
+tile/ring-depth configurations.  Prints one JSON object per measurement and a SUMMARY line.
 """
 import argparse
 import json
@@ -16,18 +18,29 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_lms_raft_llm_amd import ops  # noqa: E402
 
+TILES = {-1: "auto", 0: "32x64s6", 1: "64x64s4", 2: "128x64s3", 3: "128x128s3", 4: "64x64s2", 5: "64x128s3",
+         6: "128x128s2", 7: "64x64s6"}
 
-def timeit(fn, reps=50, inner=10):
-    for _ in range(3):
-        fn()
+
+def graph_time(fn, inner=20, reps=15):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(inner):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record()
-        for _ in range(inner):
-            fn()
+        g.replay()
         b.record()
         b.synchronize()
         ts.append(a.elapsed_time(b) * 1e3 / inner)
@@ -38,13 +51,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--batches", default="64,256,512")
+    ap.add_argument("--tiles", default="-1,1,2,3,4,5,7")
     ap.add_argument("--T", type=int, default=150)
     args = ap.parse_args()
+    L = ops.lib()
     dev = "cuda"
     d = args.d
     H = d // 64
     V = 50304
+    tiles = [int(t) for t in args.tiles.split(",")]
     res = []
+
+    def rec(**kw):
+        res.append(kw)
+        print(json.dumps(kw), flush=True)
+
     for M in [int(x) for x in args.batches.split(",")]:
         a = torch.randn(M, d, device=dev).to(torch.bfloat16)
         a4 = torch.randn(M, 4 * d, device=dev).to(torch.bfloat16)
@@ -58,7 +79,7 @@ def main():
         parts = torch.empty(8, M, d, device=dev)
         keys = torch.zeros(M, dtype=torch.int64, device=dev)
         seen = torch.zeros(M, V // 32, dtype=torch.int32, device=dev)
-        out_bf = torch.empty(M, 4 * d, dtype=torch.bfloat16, device=dev)
+        out_bf = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
         for name, (x, w) in shapes.items():
             N, K = w.shape
             variants = []
@@ -70,37 +91,40 @@ def main():
             elif name == "lmhead":
                 variants.append(("argmax", lambda x=x, w=w: ops.gemm(x, w, ops.EPI_ARGMAX, argmax_out=keys, seen=seen,
                                                                      vocab=50257, penalty=1.2)))
+                variants.append(("bf16out", lambda x=x, w=w, N=N: ops.gemm(x, w, ops.EPI_BF16, out=out_bf[:, :N])))
             else:
                 variants.append(("bf16", lambda x=x, w=w, N=N: ops.gemm(x, w, ops.EPI_BF16, out=out_bf[:, :N])))
             for vname, fn in variants:
-                med, mn = timeit(fn)
-                flops = 2 * M * N * K
-                byts = (M * K + N * K) * 2
-                res.append({"M": M, "op": name, "variant": vname, "us": round(med, 2), "us_min": round(mn, 2),
-                            "tflops": round(flops / med / 1e6, 1), "GBps": round(byts / med / 1e3, 1)})
-                print(json.dumps(res[-1]), flush=True)
-        # attention over a full-length cache
+                for t in tiles:
+                    L.dlms_gemm_force_tile(t)
+                    try:
+                        med, mn = graph_time(fn)
+                    finally:
+                        L.dlms_gemm_force_tile(-1)
+                    flops = 2 * M * N * K
+                    byts = (M * K + N * K) * 2
+                    rec(M=M, op=name, variant=vname, tile=TILES[t], us=round(med, 2), us_min=round(mn, 2),
+                        tflops=round(flops / med / 1e6, 1), GBps=round(byts / med / 1e3, 1))
         kc = torch.randn(M, H, args.T, 64, device=dev).to(torch.bfloat16)
         vc = torch.randn(M, H, args.T, 64, device=dev).to(torch.bfloat16)
         q = torch.randn(M, d, device=dev).to(torch.bfloat16)
         slot = torch.arange(M, dtype=torch.int32, device=dev)
-        for L in (32, 90, args.T):
-            kvl = torch.full((M,), L, dtype=torch.int32, device=dev)
-            o = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
-            med, mn = timeit(lambda: ops.row_attention(q, kc, vc, slot, kvl, out=o))
-            byts = M * H * L * 64 * 2 * 2
-            res.append({"M": M, "op": "attn", "variant": f"T{L}", "us": round(med, 2), "us_min": round(mn, 2),
-                        "GBps": round(byts / med / 1e3, 1)})
-            print(json.dumps(res[-1]), flush=True)
+        o = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
+        for Lk in (32, 90, args.T):
+            kvl = torch.full((M,), Lk, dtype=torch.int32, device=dev)
+            for impl in ("wave", "lds"):
+                med, mn = graph_time(lambda impl=impl: ops.row_attention(q, kc, vc, slot, kvl, out=o, impl=impl))
+                byts = M * H * Lk * 64 * 2 * 2
+                rec(M=M, op="attn", variant=f"{impl}_T{Lk}", us=round(med, 2), us_min=round(mn, 2),
+                    GBps=round(byts / med / 1e3, 1))
         x = torch.randn(M, d, device=dev)
         g = torch.ones(d, device=dev)
         b = torch.zeros(d, device=dev)
         h = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
         for s in (0, 4, 8):
-            med, mn = timeit(lambda s=s: ops.add_layernorm(x, g, b, 1e-5, parts=parts if s else None, nsplit=s,
-                                                           bias=b, out_bf16=h))
-            res.append({"M": M, "op": "add_ln", "variant": f"split{s}", "us": round(med, 2), "us_min": round(mn, 2)})
-            print(json.dumps(res[-1]), flush=True)
+            med, mn = graph_time(lambda s=s: ops.add_layernorm(x, g, b, 1e-5, parts=parts if s else None, nsplit=s,
+                                                               bias=b, out_bf16=h))
+            rec(M=M, op="add_ln", variant=f"split{s}", us=round(med, 2), us_min=round(mn, 2))
     print("SUMMARY " + json.dumps(res))
 
 

@@ -130,17 +130,18 @@ def test_layernorm(M, D):
     torch.testing.assert_close(ob.float(), ref, atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("kvlens", [[1, 5, 150], [64, 63, 65, 1024]])
-def test_row_attention(kvlens):
+@pytest.mark.parametrize("impl", ["wave", "lds"])
+@pytest.mark.parametrize("kvlens", [[1, 5, 150], [64, 63, 65, 1024], [31, 33, 7, 2]])
+def test_row_attention(kvlens, impl):
     ops = _ops()
-    H, T = 3, 1024
+    H, T = 5, 1024  # 5 heads: a partial last group of 4 heads per workgroup
     R = len(kvlens)
     q = _bf(R, H * 64, seed=11)
     kc = _bf(R, H, T, 64, seed=12)
     vc = _bf(R, H, T, 64, seed=13)
     slot = torch.arange(R, dtype=torch.int32, device=DEV).flip(0)
     kvl = torch.tensor(kvlens, dtype=torch.int32, device=DEV)
-    out = ops.row_attention(q, kc, vc, slot, kvl)
+    out = ops.row_attention(q, kc, vc, slot, kvl, impl=impl)
     for r in range(R):
         s, L = int(slot[r]), kvlens[r]
         qq = q[r].float().view(H, 64)
