@@ -124,6 +124,9 @@ class HipGPT2Engine:
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.att = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.ff = torch.zeros(B, Fl, dtype=bf, device=dev)
+        # LM-head argmax partial keys: one per (row, 64-column group) of this rank's vocab shard;
+        # zero-initialised once (columns a 128-wide tile never writes stay at the minimum key)
+        self.key_parts = torch.zeros(B, self.w.lm_head.shape[0] // 64, dtype=torch.int64, device=dev)
         self.local_keys = torch.zeros(B, dtype=torch.int64, device=dev)
         self.all_keys = torch.zeros(self.tp_size, B, dtype=torch.int64, device=dev)
         self.lens = torch.zeros(B, dtype=i32, device=dev)
@@ -147,10 +150,12 @@ class HipGPT2Engine:
             dist.all_reduce(t, group=self.tp_group)
 
     def _gather_keys(self, B: int) -> torch.Tensor:
-        """Keys of every vocab shard as [tp, B] (all-gather of 8 B per row per rank)."""
+        """Argmax keys as a [B, P] view: the LM head's per-tile partials (TP=1), or one reduced key
+        per vocab shard after an all-gather of 8 B per row per rank (TP>1)."""
         if self.tp_size > 1:
             import torch.distributed as dist
 
+            ops.argmax_reduce(self.key_parts[:B], out=self.local_keys[:B])
             flat = self.all_keys.view(-1)[: self.tp_size * B]
             if dist.get_backend(self.tp_group) == "nccl":
                 dist.all_gather_into_tensor(flat, self.local_keys[:B], group=self.tp_group)
@@ -159,8 +164,8 @@ class HipGPT2Engine:
                 dist.all_gather(parts, self.local_keys[:B].clone(), group=self.tp_group)
                 for i, p in enumerate(parts):
                     flat.view(self.tp_size, B)[i].copy_(p)
-            return flat.view(self.tp_size, B)
-        return self.local_keys[:B]
+            return flat.view(self.tp_size, B).t()
+        return self.key_parts[:B]
 
     # ------------------------------------------------------------------ transformer body
     def _split(self, M: int, N: int, K: int) -> int:
@@ -211,10 +216,10 @@ class HipGPT2Engine:
 
     def _lm_head_and_update(self, hidden_bf16: torch.Tensor, B: int, penalty: float):
         cfg = self.cfg
-        ops.gemm(hidden_bf16, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.local_keys[:B], seen=self.seen[:B],
+        ops.gemm(hidden_bf16, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[:B], seen=self.seen[:B],
                  vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
         keys = self._gather_keys(B)
-        ops.decode_update(keys, self.local_keys[:B], self.lens[:B], self.finished[:B], self.out_tokens[:B],
+        ops.decode_update(keys, self.lens[:B], self.finished[:B], self.out_tokens[:B],
                           self.seen[:B], self.cur_tok[:B], self.cur_pos[:B], self.cur_kvlen[:B], self.w.wte,
                           self.w.wpe, self.x[:B], cfg.eos_token_id, self.max_length)
 
@@ -244,11 +249,11 @@ class HipGPT2Engine:
 
     def _snapshot_state(self, B: int):
         return [t[:B].clone() for t in (self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok,
-                                        self.cur_pos, self.cur_kvlen, self.x, self.local_keys)]
+                                        self.cur_pos, self.cur_kvlen, self.x)]
 
     def _restore_state(self, B: int, saved):
         for t, s in zip((self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
-                         self.cur_kvlen, self.x, self.local_keys), saved):
+                         self.cur_kvlen, self.x), saved):
             t[:B].copy_(s)
 
     # ------------------------------------------------------------------ prefill
@@ -282,7 +287,6 @@ class HipGPT2Engine:
         self.seen[:B].copy_(seen, non_blocking=True)
         self.lens[:B].copy_(lens_t, non_blocking=True)
         self.finished[:B].copy_(fin, non_blocking=True)
-        self.local_keys[:B].zero_()
 
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         f32, bf = torch.float32, torch.bfloat16

@@ -89,7 +89,9 @@ def _bind(L):
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
-        "dlms_decode_update": [P, I, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I, I, P],
+        "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I,
+                               I, P],
+        "dlms_argmax_reduce": [P, I, ctypes.c_longlong, P, I, P],
         "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
         "dlms_mean_pool": [P, P, P, P, I, I, P],
         "dlms_cosine": [P, P, P, I, I, I, F, P],
@@ -215,11 +217,14 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
             raise ValueError("partial out too small")
         ep.out, ep.ldo, ep.split_k, ep.split_stride = out.data_ptr(), out.stride(1), split_k, out.stride(0)
     elif epi == EPI_ARGMAX:
-        _req(argmax_out, torch.int64, "argmax_out", 1)
+        # argmax_out: int64 [M, >= N/64] partial keys, one per (row, 64-column group of tile starts);
+        # columns never written must be zero-initialised once (0 is the minimum key)
+        _req(argmax_out, torch.int64, "argmax_out", 2)
         _req(seen, torch.int32, "seen", 2)
-        if argmax_out.numel() < M or seen.shape[0] < M or seen.shape[1] * 32 < vocab:
-            raise ValueError("argmax epilogue buffers too small")
-        ep.argmax_out, ep.seen = argmax_out.data_ptr(), seen.data_ptr()
+        if argmax_out.shape[0] < M or argmax_out.shape[1] < N // 64 or seen.shape[0] < M or \
+                seen.shape[1] * 32 < vocab or col_offset % 64:
+            raise ValueError("argmax epilogue buffers too small / misaligned shard")
+        ep.argmax_out, ep.ldo, ep.seen = argmax_out.data_ptr(), argmax_out.stride(0), seen.data_ptr()
         ep.seen_words, ep.vocab, ep.col_offset, ep.penalty = seen.stride(0), vocab, col_offset, penalty
         out = argmax_out
     else:
@@ -342,12 +347,26 @@ def embed(tokens: torch.Tensor, positions: torch.Tensor, wte: torch.Tensor, wpe:
     return out
 
 
-def decode_update(keys: torch.Tensor, local_keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok, cur_pos,
-                  cur_kvlen, wte, wpe, x, eos: int, t_max: int):
-    _req(keys, torch.int64, "keys")
-    _req(local_keys, torch.int64, "local_keys", 1)
-    B = local_keys.numel()
-    world = keys.numel() // B
+def argmax_reduce(parts: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """[B, P] partial argmax keys -> [B] (max per row)."""
+    _req(parts, torch.int64, "parts", 2)
+    B, P = parts.shape
+    if out is None:
+        out = torch.empty(B, dtype=torch.int64, device=parts.device)
+    _req(out, torch.int64, "out", 1)
+    if out.numel() < B:
+        raise ValueError("argmax_reduce: out too short")
+    _check(lib().dlms_argmax_reduce(_p(parts), P, parts.stride(0), _p(out), B, _stream()), "dlms_argmax_reduce")
+    return out
+
+
+def decode_update(keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok, cur_pos, cur_kvlen, wte, wpe, x,
+                  eos: int, t_max: int):
+    """keys: int64 [B, P] (row-major partial keys) or a transposed view [P, B].T (gathered per-rank
+    keys); the token of row b is the argmax over its P keys."""
+    if keys.dtype != torch.int64 or keys.device.type != "cuda" or keys.dim() != 2:
+        raise ValueError("decode_update: keys must be a 2-D int64 GPU tensor")
+    B, P = keys.shape
     for t, n in ((lens, "lens"), (finished, "finished"), (cur_tok, "cur_tok"), (cur_pos, "cur_pos"),
                  (cur_kvlen, "cur_kvlen")):
         _req(t, torch.int32, n, 1)
@@ -359,7 +378,7 @@ def decode_update(keys: torch.Tensor, local_keys: torch.Tensor, lens, finished, 
     D = wte.shape[1]
     if out_tokens.shape[0] < B or x.shape[0] < B or x.shape[1] < D:
         raise ValueError("decode_update: buffers too small")
-    _check(lib().dlms_decode_update(_p(keys), world, _p(local_keys), _p(lens), _p(finished), _p(out_tokens),
+    _check(lib().dlms_decode_update(_p(keys), P, keys.stride(0), keys.stride(1), _p(lens), _p(finished), _p(out_tokens),
                                     out_tokens.stride(0), _p(seen), seen.stride(0), _p(cur_tok), _p(cur_pos),
                                     _p(cur_kvlen), _p(wte), _p(wpe), _p(x), x.stride(0), B, D, eos, t_max, _stream()),
            "dlms_decode_update")

@@ -24,15 +24,41 @@ __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ toke
     }
 }
 
+// max over a row's partial argmax keys, one wave per row (keys(b, p) = keys[b * sb + p * sp])
+__device__ __forceinline__ unsigned long long wave_key_max(const unsigned long long* __restrict__ keys, int b,
+                                                           int nparts, long long sb, long long sp, int lane) {
+    unsigned long long best = 0ull;
+    for (int p = lane; p < nparts; p += 64) {
+        const unsigned long long k = keys[(size_t)b * sb + (size_t)p * sp];
+        best = k > best ? k : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long k = __shfl_xor(best, o, 64);
+        best = k > best ? k : best;
+    }
+    return best;
+}
+
+// argmax partials [B][nparts] -> one key per row (before the cross-rank all-gather under TP)
+__global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long long* __restrict__ keys, int nparts,
+                                                            long long sb, unsigned long long* out, int B) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const unsigned long long best = wave_key_max(keys, b, nparts, sb, 1, lane);
+    if (lane == 0) out[b] = best;
+}
+
 // One wave per live sequence b.
-//   keys[w][b]   packed (ordered value, ~index) argmax keys from each of `world` vocab shards
+//   keys(b, p)   packed (ordered value, ~index) argmax keys: the LM head's per-column-tile
+//                partials (TP=1) or the all-gathered per-rank keys (TP>1); max over p
 //   lens[b]      tokens so far (prompt + generated);  finished[b] stop flag
 //   out_tokens   [B][max_len] full sequences (prompt already written by the host)
 //   seen         [B][seen_words] repetition-penalty bitmap
-// Writes the next forward's token/position/kv-length for row b, its embedding into x, and clears
-// the local argmax slot for the next LM-head pass.
-__global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long long* __restrict__ keys, int world,
-                                                            unsigned long long* local_keys, int* lens, int* finished,
+// Writes the next forward's token/position/kv-length for row b and its embedding into x.
+__global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long long* __restrict__ keys, int nparts,
+                                                            long long sb, long long sp, int* lens, int* finished,
                                                             int* out_tokens, int max_len, unsigned int* seen,
                                                             int seen_words, int* cur_tok, int* cur_pos, int* cur_kvlen,
                                                             const bf16_t* __restrict__ wte,
@@ -41,14 +67,9 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= B) return;
+    const unsigned long long best = wave_key_max(keys, b, nparts, sb, sp, lane);
     int tok = 0, pos = 0;
     if (lane == 0) {
-        unsigned long long best = 0ull;
-        for (int w = 0; w < world; ++w) {
-            const unsigned long long k = keys[(size_t)w * B + b];
-            best = k > best ? k : best;
-        }
-        local_keys[b] = 0ull;
         int len = lens[b];
         if (!finished[b]) {
             // best == 0 means no shard produced a candidate (cannot happen for vocab >= 1); stay in
@@ -90,15 +111,22 @@ extern "C" hipError_t dlms_embed(const int* tokens, const int* positions, const 
     return hipGetLastError();
 }
 
-extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int world, unsigned long long* local_keys,
+extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int nparts, long long sb, long long sp,
                                          int* lens, int* finished, int* out_tokens, int max_len, unsigned int* seen,
                                          int seen_words, int* cur_tok, int* cur_pos, int* cur_kvlen, const void* wte,
                                          const void* wpe, float* x, int ldx, int B, int D, int eos, int t_max,
                                          hipStream_t stream) {
-    if (D % 8 != 0 || B <= 0 || world <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, world, local_keys, lens,
+    if (D % 8 != 0 || B <= 0 || nparts <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, sp, lens,
                        finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
                        reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, B, D, eos,
                        t_max);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t dlms_argmax_reduce(const unsigned long long* keys, int nparts, long long sb,
+                                         unsigned long long* out, int B, hipStream_t stream) {
+    if (B <= 0 || nparts <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(argmax_reduce_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, out, B);
     return hipGetLastError();
 }

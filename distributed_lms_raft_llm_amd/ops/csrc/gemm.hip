@@ -163,45 +163,59 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
     const int col_base = n0 + wn * WTN + (lane & 15);
 
     if constexpr (EPI == EPI_ARGMAX) {
-        unsigned long long best[TM][4];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) best[i][r] = 0ull;
+        // Fused repetition penalty + argmax (K11/K12).  The block's BM x BN slice of the seen
+        // bitmap is staged in LDS (BN/32 words per row; tile columns are 32-aligned), each row's
+        // best (ordered value, ~index) key is reduced across lanes by shuffles and across the WN
+        // column-waves through LDS, and ONE key per (row, column tile) is stored -- no atomics.
+        // The consumer (decode_update / argmax_reduce) takes the max over the tiles of a row.
+        constexpr int WPR = BN / 32;  // bitmap words per tile row
+        unsigned int* sbits = reinterpret_cast<unsigned int*>(smem);
+        unsigned long long* sred = reinterpret_cast<unsigned long long*>(smem + BM * WPR * 4 + 16);
+        __syncthreads();  // every wave is done reading the last ring stage
+        const int wbase = (n0 + ep.col_offset) >> 5;
+        for (int e = tid; e < BM * WPR; e += 256) {
+            const int r = e / WPR, w = e % WPR;
+            const int row = m0 + r < M ? m0 + r : M - 1;
+            const int word = wbase + w;
+            sbits[e] = word < ep.seen_words ? ep.seen[(size_t)row * ep.seen_words + word] : 0u;
+        }
+        __syncthreads();
+        const int lrow0 = wm * WTM + (lane >> 4) * 4;
+        const int lcol0 = wn * WTN + (lane & 15);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = row_base + i * 16 + r;
-                if (row >= M) continue;
-                const unsigned int* srow = ep.seen + (size_t)row * ep.seen_words;
+                const int lr = lrow0 + i * 16 + r;
+                unsigned long long b = 0ull;
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-                    const int col = col_base + j * 16;
-                    const int gcol = col + ep.col_offset;
-                    if (gcol >= ep.vocab) continue;
+                    const int lc = lcol0 + j * 16;
+                    const int gcol = n0 + lc + ep.col_offset;
                     float v = acc[i][j][r];
-                    if ((srow[gcol >> 5] >> (gcol & 31)) & 1u) v = v < 0.f ? v * ep.penalty : v / ep.penalty;
+                    if ((sbits[lr * WPR + (lc >> 5)] >> (lc & 31)) & 1u) v = v < 0.f ? v * ep.penalty : v / ep.penalty;
                     const unsigned long long key =
                         ((unsigned long long)f32_ordered(v) << 32) | (unsigned long long)(~(unsigned int)gcol);
-                    best[i][r] = key > best[i][r] ? key : best[i][r];
+                    b = (gcol < ep.vocab && key > b) ? key : b;
                 }
-            }
-        }
-        // reduce across the 16 lanes that share rows (lane bits 0..3 = column)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                unsigned long long b = best[i][r];
 #pragma unroll
                 for (int o = 1; o < 16; o <<= 1) {
-                    unsigned long long other = __shfl_xor(b, o, 64);
+                    const unsigned long long other = __shfl_xor(b, o, 64);
                     b = other > b ? other : b;
                 }
-                const int row = row_base + i * 16 + r;
-                if ((lane & 15) == 0 && row < M && b != 0ull) atomicMax(ep.argmax_out + row, b);
+                if ((lane & 15) == 0) sred[wn * BM + lr] = b;
             }
+        }
+        __syncthreads();
+        for (int lr = tid; lr < BM; lr += 256) {
+            unsigned long long b = sred[lr];
+#pragma unroll
+            for (int w = 1; w < WN; ++w) {
+                const unsigned long long o = sred[w * BM + lr];
+                b = o > b ? o : b;
+            }
+            if (m0 + lr < M) ep.argmax_out[(size_t)(m0 + lr) * ep.ldo + (n0 >> 6)] = b;
+        }
         return;
     }
 

@@ -106,8 +106,9 @@ def test_gemm_argmax_penalty():
     for bit in range(32):
         words |= seen_bool.view(M, Vp // 32, 32)[:, :, bit].long() << bit
     seen.copy_(words.to(torch.int64).where(words < 2**31, words - 2**32).to(torch.int32))
-    keys = torch.zeros(M, dtype=torch.int64, device=DEV)
-    ops.gemm(a, w, ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2)
+    parts = torch.zeros(M, Vp // 64, dtype=torch.int64, device=DEV)
+    ops.gemm(a, w, ops.EPI_ARGMAX, argmax_out=parts, seen=seen, vocab=V, penalty=1.2)
+    keys = ops.argmax_reduce(parts)
     pen = torch.where(logits < 0, logits * 1.2, logits / 1.2)
     ref = torch.where(seen_bool, pen, logits)[:, :V]
     got = (~(keys & 0xFFFFFFFF)).bitwise_and(0xFFFFFFFF)
@@ -176,12 +177,23 @@ def test_embed_and_decode_update():
     seen = torch.zeros(B, 32, dtype=torch.int32, device=DEV)
     ct, cp, ck = (torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(3))
     xb = torch.zeros(B, D, device=DEV)
-    ops.decode_update(keys, keys, lens, fin, out, seen, ct, cp, ck, wte, wpe, xb, eos=999, t_max=T)
+    # keys as [B, P] partials with a decoy partial per row (max must win), and as a [P, B].T view
+    decoy = torch.tensor([key(-5.0, 1)] * B, dtype=torch.int64, device=DEV)
+    parts = torch.stack([decoy, keys], dim=1)
+    keys_t = torch.stack([keys, decoy], dim=0).t()
+    assert keys_t.stride(0) == 1
+    ops.decode_update(parts, lens, fin, out, seen, ct, cp, ck, wte, wpe, xb, eos=999, t_max=T)
     assert lens.tolist() == [5, 10, 10]
     assert fin.tolist() == [0, 1, 1]
     assert out[0, 4].item() == 17 and out[1, 9].item() == 999
     assert ct.tolist() == [17, 999, 42] and cp.tolist() == [4, 9, 9] and ck.tolist() == [5, 10, 10]
-    assert keys.tolist() == [0, 0, 0]
+    # the transposed (gathered-per-rank) layout decodes the same tokens
+    lens2 = torch.tensor([4, 9, 10], dtype=torch.int32, device=DEV)
+    fin2 = torch.tensor([0, 0, 1], dtype=torch.int32, device=DEV)
+    out2 = torch.zeros(B, T, dtype=torch.int32, device=DEV)
+    out2[2, 9] = 42
+    ops.decode_update(keys_t, lens2, fin2, out2, torch.zeros_like(seen), ct, cp, ck, wte, wpe, xb, eos=999, t_max=T)
+    assert torch.equal(out2, out) and lens2.tolist() == lens.tolist()
     assert (seen[0, 0].item() >> 17) & 1 == 1
     torch.testing.assert_close(xb[0], wte[17].float() + wpe[4].float())
 
