@@ -89,8 +89,8 @@ def _bind(L):
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
-        "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, I, P, I, P, P, P, P, P, P, I, I, I, I,
-                               I, P],
+        "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I,
+                               I, I, I, P],
         "dlms_argmax_reduce": [P, I, ctypes.c_longlong, P, I, P],
         "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
         "dlms_mean_pool": [P, P, P, P, I, I, P],
@@ -361,24 +361,32 @@ def argmax_reduce(parts: torch.Tensor, out: torch.Tensor | None = None) -> torch
 
 
 def decode_update(keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok, cur_pos, cur_kvlen, wte, wpe, x,
-                  eos: int, t_max: int):
-    """keys: int64 [B, P] (row-major partial keys) or a transposed view [P, B].T (gathered per-rank
-    keys); the token of row b is the argmax over its P keys."""
+                  eos: int, t_max: int, slot_map: torch.Tensor | None = None):
+    """keys: int64 [R, P] (row-major partial keys) or a transposed view [P, R].T (gathered per-rank
+    keys); the token of row i is the argmax over its P keys and updates sequence slot
+    ``slot_map[i]`` (default: slot i)."""
     if keys.dtype != torch.int64 or keys.device.type != "cuda" or keys.dim() != 2:
         raise ValueError("decode_update: keys must be a 2-D int64 GPU tensor")
     B, P = keys.shape
+    nslots = B
+    if slot_map is not None:
+        _req(slot_map, torch.int32, "slot_map", 1)
+        if slot_map.numel() < B:
+            raise ValueError("slot_map too short")
+        nslots = lens.numel()  # callers guarantee every slot_map entry is < the state capacity
     for t, n in ((lens, "lens"), (finished, "finished"), (cur_tok, "cur_tok"), (cur_pos, "cur_pos"),
                  (cur_kvlen, "cur_kvlen")):
         _req(t, torch.int32, n, 1)
-        if t.numel() < B:
+        if t.numel() < nslots:
             raise ValueError(f"{n} too short")
     _req(out_tokens, torch.int32, "out_tokens", 2)
     _req(seen, torch.int32, "seen", 2)
     _req(x, torch.float32, "x", 2)
     D = wte.shape[1]
-    if out_tokens.shape[0] < B or x.shape[0] < B or x.shape[1] < D:
+    if out_tokens.shape[0] < nslots or x.shape[0] < nslots or x.shape[1] < D or seen.shape[0] < nslots:
         raise ValueError("decode_update: buffers too small")
-    _check(lib().dlms_decode_update(_p(keys), P, keys.stride(0), keys.stride(1), _p(lens), _p(finished), _p(out_tokens),
+    _check(lib().dlms_decode_update(_p(keys), P, keys.stride(0), keys.stride(1), _p(slot_map), _p(lens), _p(finished),
+                                    _p(out_tokens),
                                     out_tokens.stride(0), _p(seen), seen.stride(0), _p(cur_tok), _p(cur_pos),
                                     _p(cur_kvlen), _p(wte), _p(wpe), _p(x), x.stride(0), B, D, eos, t_max, _stream()),
            "dlms_decode_update")

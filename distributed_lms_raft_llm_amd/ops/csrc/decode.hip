@@ -57,17 +57,22 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
 //   out_tokens   [B][max_len] full sequences (prompt already written by the host)
 //   seen         [B][seen_words] repetition-penalty bitmap
 // Writes the next forward's token/position/kv-length for row b and its embedding into x.
+// slot_map (optional): key row i updates sequence slot slot_map[i] -- used when a prefill of new
+// requests lands in arbitrary free slots of a running continuous batch.
 __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long long* __restrict__ keys, int nparts,
-                                                            long long sb, long long sp, int* lens, int* finished,
-                                                            int* out_tokens, int max_len, unsigned int* seen,
-                                                            int seen_words, int* cur_tok, int* cur_pos, int* cur_kvlen,
+                                                            long long sb, long long sp,
+                                                            const int* __restrict__ slot_map, int* lens,
+                                                            int* finished, int* out_tokens, int max_len,
+                                                            unsigned int* seen, int seen_words, int* cur_tok,
+                                                            int* cur_pos, int* cur_kvlen,
                                                             const bf16_t* __restrict__ wte,
                                                             const bf16_t* __restrict__ wpe, float* x, int ldx, int B,
                                                             int D, int eos, int t_max) {
     const int lane = threadIdx.x & 63;
-    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= B) return;
-    const unsigned long long best = wave_key_max(keys, b, nparts, sb, sp, lane);
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= B) return;
+    const unsigned long long best = wave_key_max(keys, i, nparts, sb, sp, lane);
+    const int b = slot_map ? slot_map[i] : i;
     int tok = 0, pos = 0;
     if (lane == 0) {
         int len = lens[b];
@@ -112,13 +117,13 @@ extern "C" hipError_t dlms_embed(const int* tokens, const int* positions, const 
 }
 
 extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int nparts, long long sb, long long sp,
-                                         int* lens, int* finished, int* out_tokens, int max_len, unsigned int* seen,
-                                         int seen_words, int* cur_tok, int* cur_pos, int* cur_kvlen, const void* wte,
-                                         const void* wpe, float* x, int ldx, int B, int D, int eos, int t_max,
-                                         hipStream_t stream) {
+                                         const int* slot_map, int* lens, int* finished, int* out_tokens, int max_len,
+                                         unsigned int* seen, int seen_words, int* cur_tok, int* cur_pos,
+                                         int* cur_kvlen, const void* wte, const void* wpe, float* x, int ldx, int B,
+                                         int D, int eos, int t_max, hipStream_t stream) {
     if (D % 8 != 0 || B <= 0 || nparts <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, sp, lens,
-                       finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
+    hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, sp, slot_map,
+                       lens, finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
                        reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, B, D, eos,
                        t_max);
     return hipGetLastError();

@@ -46,10 +46,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 // in-flight DMA every step); out-of-range A rows read a clamped valid row (their results are never
 // stored), so the DMA never needs predication.
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
-__global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__ A, int lda,
+__global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __restrict__ A, int lda,
                                                       const bf16_t* __restrict__ W, int ldw, int M, int N,
                                                       int K, GemmEpi ep) {
-    static_assert(WM * WN == 4, "4 waves per workgroup");
+    constexpr int NW = WM * WN;  // waves per workgroup (4 or 8)
+    constexpr int NT = 64 * NW;
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves per workgroup");
     constexpr int WTM = BM / WM;  // rows per wave
     constexpr int WTN = BN / WN;  // cols per wave
     constexpr int TM = WTM / 16;
@@ -59,8 +61,8 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
     constexpr int A_BYTES = BM * ROWB;
     constexpr int STAGE_BYTES = (BM + BN) * ROWB;
     constexpr int PIECES = STAGE_BYTES / 1024;
-    static_assert(PIECES % 4 == 0, "(BM + BN) must be a multiple of 32");
-    constexpr int PPW = PIECES / 4;  // LDS-DMA instructions per wave per stage
+    static_assert(PIECES % NW == 0, "(BM + BN) * 128 B must split evenly into 1-KiB pieces per wave");
+    constexpr int PPW = PIECES / NW;  // LDS-DMA instructions per wave per stage
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
     const bf16_t* src[PPW];
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-        const int piece = wave + 4 * i;
+        const int piece = wave + NW * i;
         const int row = piece * 8 + (lane >> 3);
         const int lchunk = (lane & 7) ^ (lane >> 3);
         if (row < BM) {
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
         char* dst = smem + stage * STAGE_BYTES;
 #pragma unroll
         for (int i = 0; i < PPW; ++i)
-            __builtin_amdgcn_global_load_lds((glob_void_t*)(src[i] + k0), (lds_void_t*)(dst + (wave + 4 * i) * 1024),
+            __builtin_amdgcn_global_load_lds((glob_void_t*)(src[i] + k0), (lds_void_t*)(dst + (wave + NW * i) * 1024),
                                              16, 0, 0);
     };
 
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
         unsigned long long* sred = reinterpret_cast<unsigned long long*>(smem + BM * WPR * 4 + 16);
         __syncthreads();  // every wave is done reading the last ring stage
         const int wbase = (n0 + ep.col_offset) >> 5;
-        for (int e = tid; e < BM * WPR; e += 256) {
+        for (int e = tid; e < BM * WPR; e += NT) {
             const int r = e / WPR, w = e % WPR;
             const int row = m0 + r < M ? m0 + r : M - 1;
             const int word = wbase + w;
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const bf16_t* __restrict__
             }
         }
         __syncthreads();
-        for (int lr = tid; lr < BM; lr += 256) {
+        for (int lr = tid; lr < BM; lr += NT) {
             unsigned long long b = sred[lr];
 #pragma unroll
             for (int w = 1; w < WN; ++w) {
@@ -272,7 +274,8 @@ static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI>), dim3(tiles), dim3(256), lds, stream, A, lda, W,
+    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI>), dim3(tiles), dim3(64 * WM * WN), lds, stream, A,
+                       lda, W,
                        ldw, M, N, K, ep);
     return hipGetLastError();
 }
@@ -299,9 +302,14 @@ static hipError_t launch_forced(int id, const bf16_t* A, int lda, const bf16_t* 
             case 3: return launch_gemm_cfg<128, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
             case 5: return launch_gemm_cfg<64, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
             case 6: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            // 8-wave workgroups: two waves per SIMD, one's LDS reads under the other's MFMAs
+            case 8: return launch_gemm_cfg<256, 128, 4, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 10: return launch_gemm_cfg<128, 128, 4, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 11: return launch_gemm_cfg<128, 128, 2, 4, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
             default: break;
         }
     }
+    if (N % 256 == 0 && id == 9) return launch_gemm_cfg<128, 256, 2, 4, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     *done = false;
     return hipSuccess;
 }

@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_lms_raft_llm_amd import ops  # noqa: E402
 
 TILES = {-1: "auto", 0: "32x64s6", 1: "64x64s4", 2: "128x64s3", 3: "128x128s3", 4: "64x64s2", 5: "64x128s3",
-         6: "128x128s2", 7: "64x64s6"}
+         6: "128x128s2", 7: "64x64s6", 8: "256x128w8s2", 9: "128x256w8s2", 10: "128x128w8s3(4x2)",
+         11: "128x128w8s3(2x4)"}
 
 
 def graph_time(fn, inner=20, reps=15):
@@ -77,7 +78,7 @@ def main():
             "lmhead": (a, torch.randn(V, d, device=dev).to(torch.bfloat16) * 0.02),
         }
         parts = torch.empty(8, M, d, device=dev)
-        keys = torch.zeros(M, dtype=torch.int64, device=dev)
+        keys = torch.zeros(M, V // 64, dtype=torch.int64, device=dev)
         seen = torch.zeros(M, V // 32, dtype=torch.int32, device=dev)
         out_bf = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
         for name, (x, w) in shapes.items():
