@@ -129,7 +129,7 @@ class HipGPT2Engine:
         self.key_parts = torch.zeros(B, self.w.lm_head.shape[0] // 64, dtype=torch.int64, device=dev)
         self.local_keys = torch.zeros(B, dtype=torch.int64, device=dev)
         self.all_keys = torch.zeros(self.tp_size, B, dtype=torch.int64, device=dev)
-        self.lens = torch.zeros(B, dtype=i32, device=dev)
+        self.lens = torch.ones(B, dtype=i32, device=dev)  # every slot starts inert (see _reset_slots)
         self.finished = torch.ones(B, dtype=i32, device=dev)
         self.out_tokens = torch.zeros(B, T, dtype=i32, device=dev)
         self.seen_words = cfg.vocab_padded // 32
@@ -138,6 +138,7 @@ class HipGPT2Engine:
         self.cur_pos = torch.zeros(B, dtype=i32, device=dev)
         self.cur_kvlen = torch.ones(B, dtype=i32, device=dev)
         self.slots = torch.arange(B, dtype=i32, device=dev)
+        self._reset_slots(0, B)
 
     def kv_cache_bytes(self) -> int:
         return self.kv.numel() * self.kv.element_size()
@@ -169,16 +170,19 @@ class HipGPT2Engine:
 
     # ------------------------------------------------------------------ transformer body
     def _split(self, M: int, N: int, K: int) -> int:
-        """Split-K factor for a row-parallel projection (N = d): decode GEMMs are latency-bound, so
-        slice K until the grid covers the CUs, keeping >= 3 K-steps per slice."""
-        if self.tp_size > 1 or M > 512:
+        """Split-K factor for a row-parallel projection (N = d): slice K until the grid covers the
+        CUs (<= 1024 workgroups), keeping >= 3 K-steps per slice (>= 6 above M = 512, where the
+        extra partial slabs the add+LayerNorm re-reads start to cost).  Fit to the tile sweep
+        (profiles/r1_gemm_tile_sweep.jsonl): M=1024 c_proj split 4 10.4 us vs unsplit 17 us."""
+        if self.tp_size > 1:
             return 1
-        bm = 16 if M <= 16 else 32 if M <= 32 else 64
+        bm = 32 if M <= 32 else 64
         tiles = -(-M // bm) * (N // 64)
         ksteps = K // 64
+        min_steps = 3 if M <= 512 else 6
         best = 1
         for s in (2, 3, 4, 6, 8):
-            if ksteps % s == 0 and tiles * s <= 512 and ksteps // s >= 3:
+            if ksteps % s == 0 and tiles * s <= 1024 and ksteps // s >= min_steps:
                 best = s
         return best
 
@@ -257,36 +261,54 @@ class HipGPT2Engine:
             t[:B].copy_(s)
 
     # ------------------------------------------------------------------ prefill
-    def _prefill(self, prompts: list[list[int]], B: int, penalty: float):
+    def _reset_slots(self, lo: int, hi: int):
+        """Make slots [lo, hi) inert: finished, one EOS token, position 0 (decode replays over a
+        bucket touch them harmlessly and decode_update leaves them alone)."""
+        if hi <= lo:
+            return
+        self.lens[lo:hi].fill_(1)
+        self.finished[lo:hi].fill_(1)
+        self.out_tokens[lo:hi, 0].fill_(self.cfg.eos_token_id)
+        self.cur_tok[lo:hi].fill_(self.cfg.eos_token_id)
+        self.cur_pos[lo:hi].zero_()
+        self.cur_kvlen[lo:hi].fill_(1)
+
+    def _prefill_into(self, prompts: list[list[int]], slots: list[int], penalty: float):
+        """Packed variable-length prefill of ``prompts`` into KV-cache slots ``slots`` (any free
+        slots of a running batch), then the first greedy token of each: the LM head's argmax rows
+        map back to their slots through decode_update's slot map."""
         cfg, dev = self.cfg, self.device
         n = len(prompts)
+        if n != len(slots) or n == 0:
+            raise ValueError("prefill: one slot per prompt")
+        if min(slots) < 0 or max(slots) >= self.max_batch or len(set(slots)) != n:
+            raise ValueError(f"prefill: slots must be distinct and in [0, {self.max_batch})")
+        T = self.max_length
         lens = [len(p) for p in prompts]
+        if min(lens) < 1 or max(lens) > T:
+            raise ValueError("prefill: prompt lengths must be in [1, max_length]")
         R = sum(lens)
         tokens = torch.tensor([t for p in prompts for t in p], dtype=torch.int32)
         pos = torch.tensor([i for L in lens for i in range(L)], dtype=torch.int32)
-        slot = torch.tensor([b for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32)
-        last = torch.tensor([sum(lens[: b + 1]) - 1 for b in range(n)] + [R - 1] * (B - n), dtype=torch.int32)
-        tokens_d, pos_d, slot_d = (t.to(dev, non_blocking=True) for t in (tokens, pos, slot))
-        kvlen_d = pos_d + 1
-        last_d = last.to(dev, non_blocking=True)
+        slot = torch.tensor([slots[b] for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32)
+        last = torch.tensor(np.cumsum(lens) - 1, dtype=torch.int32)
 
-        # host-side sequence state for the batch bucket (rows >= n are inert: finished)
-        T = self.max_length
-        out_tok = torch.zeros(B, T, dtype=torch.int32)
-        seen = torch.zeros(B, self.seen_words, dtype=torch.int32)
-        lens_t = torch.ones(B, dtype=torch.int32)
-        fin = torch.ones(B, dtype=torch.int32)
+        # host-built per-sequence state, scattered into the chosen slots
+        out_tok = torch.zeros(n, T, dtype=torch.int32)
+        seen = torch.zeros(n, self.seen_words, dtype=torch.int32)
         for b, p in enumerate(prompts):
             out_tok[b, : len(p)] = torch.tensor(p, dtype=torch.int32)
             seen[b] = torch.from_numpy(seen_bitmap(p, self.seen_words))
-            lens_t[b] = len(p)
-            fin[b] = 1 if len(p) >= T else 0
-        for b in range(n, B):
-            out_tok[b, 0] = cfg.eos_token_id
-        self.out_tokens[:B].copy_(out_tok, non_blocking=True)
-        self.seen[:B].copy_(seen, non_blocking=True)
-        self.lens[:B].copy_(lens_t, non_blocking=True)
-        self.finished[:B].copy_(fin, non_blocking=True)
+        lens_t = torch.tensor(lens, dtype=torch.int32)
+        fin = (lens_t >= T).to(torch.int32)
+        tokens_d, pos_d, slot_d, last_d, slots_d, out_d, seen_d, lens_d, fin_d = (
+            t.to(dev, non_blocking=True)
+            for t in (tokens, pos, slot, last, torch.tensor(slots, dtype=torch.int32), out_tok, seen, lens_t, fin))
+        idx = slots_d.long()
+        self.out_tokens.index_copy_(0, idx, out_d)
+        self.seen.index_copy_(0, idx, seen_d)
+        self.lens.index_copy_(0, idx, lens_d)
+        self.finished.index_copy_(0, idx, fin_d)
 
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         f32, bf = torch.float32, torch.bfloat16
@@ -297,9 +319,19 @@ class HipGPT2Engine:
         q = torch.empty(R, Dl, dtype=bf, device=dev)
         att = torch.empty(R, Dl, dtype=bf, device=dev)
         ff = torch.empty(R, Fl, dtype=bf, device=dev)
-        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, kvlen_d, R, final_h=None)
+        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None)
         hl = ops.layernorm_gather(x, last_d, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon)
-        self._lm_head_and_update(hl, B, penalty)
+        # first token: argmax rows are prompts (seen rows gathered), updates land in their slots
+        ops.gemm(hl, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[:n], seen=seen_d,
+                 vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
+        keys = self._gather_keys(n)
+        ops.decode_update(keys, self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
+                          self.cur_kvlen, self.w.wte, self.w.wpe, self.x, cfg.eos_token_id, T, slot_map=slots_d)
+
+    def _prefill(self, prompts: list[list[int]], B: int, penalty: float):
+        """Static batch: prompts into slots [0, n), slots [n, B) inert."""
+        self._reset_slots(len(prompts), B)
+        self._prefill_into(prompts, list(range(len(prompts))), penalty)
 
     @torch.no_grad()
     def prefill_last_hidden(self, prompts: list[list[int]]) -> torch.Tensor:
@@ -319,6 +351,36 @@ class HipGPT2Engine:
         h, q, att, ff = (torch.empty(R, n, dtype=bf, device=dev) for n in (D, Dl, Dl, Fl))
         self._layers(x, parts, h, q, att, ff, slot, pos, pos + 1, R, final_h=None)
         return ops.layernorm_gather(x, last, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon).float()
+
+    # ------------------------------------------------------------------ slot API (continuous batching)
+    @torch.no_grad()
+    def admit(self, prompts: list[list[int]], slots: list[int], repetition_penalty: float = 1.2):
+        """Prefill new sequences into free ``slots`` of the running batch (first token included)."""
+        self._prefill_into([list(p) for p in prompts], list(slots), repetition_penalty)
+
+    @torch.no_grad()
+    def decode(self, B: int, steps: int, repetition_penalty: float = 1.2):
+        """``steps`` greedy decode steps over slots [0, B) (finished/inert slots are no-ops)."""
+        if B > self.max_batch or B not in (_bucket(B), self.max_batch):
+            raise ValueError(f"decode: batch bucket {B} invalid")
+        graph = self._graph_for(B, repetition_penalty) if self.use_graph else None
+        for _ in range(steps):
+            if graph is not None:
+                graph.replay()
+            else:
+                self._decode_step(B, repetition_penalty)
+
+    def finished_flags(self, B: int) -> list[int]:
+        return self.finished[:B].cpu().tolist()
+
+    def collect(self, slots: list[int]) -> list[list[int]]:
+        """Token sequences (prompt + generated) of ``slots``."""
+        if not slots:
+            return []
+        idx = torch.tensor(slots, dtype=torch.long, device=self.device)
+        lens = self.lens.index_select(0, idx).cpu().tolist()
+        toks = self.out_tokens.index_select(0, idx).cpu()
+        return [toks[i, : lens[i]].tolist() for i in range(len(slots))]
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()

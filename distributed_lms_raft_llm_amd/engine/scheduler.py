@@ -1,0 +1,149 @@
+"""Continuous (in-flight) batching scheduler for the tutoring decode engine.
+
+The reference serves one ``model.generate`` per request (SURVEY.md §3.3,
+reference ``tutoring_server.py``: GetLLMAnswer -> tokenizer -> generate(max_length=150)),
+so concurrent students queue behind each other.  Here one scheduler thread owns the engine's
+KV-cache slots: a request is prefilled into the lowest free slot as soon as one exists (packed
+varlen prefill, ``HipGPT2Engine.admit``), every live sequence advances together in graph-replayed
+decode chunks over the smallest batch bucket covering the occupied slots, and a finished
+sequence frees its slot at the next chunk boundary -- so a late request never waits for an
+earlier batch to drain.
+
+Engine protocol (``HipGPT2Engine`` implements it; tests use a CPU fake):
+    max_batch, max_length, cfg.eos_token_id
+    admit(prompts, slots, repetition_penalty)   prefill + first token into those slots
+    decode(B, steps, repetition_penalty)        ``steps`` decode steps over slots [0, B)
+    finished_flags(B) -> list[int]              per-slot stop flags
+    collect(slots) -> list[list[int]]           prompt + generated tokens
+"""
+from __future__ import annotations
+
+import heapq
+import threading
+import time
+from collections import deque
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+
+import torch
+
+from ..utils.metrics import METRICS
+from .gpt2_engine import _bucket
+
+
+@dataclass
+class _Req:
+    prompt: list[int]
+    future: Future
+    t_submit: float = field(default_factory=time.perf_counter)
+
+
+class ContinuousBatcher:
+    def __init__(self, engine, repetition_penalty: float = 1.2, chunk: int = 8, max_admit: int | None = None,
+                 name: str = "tutor"):
+        self.engine = engine
+        self.penalty = float(repetition_penalty)
+        self.chunk = max(1, int(chunk))
+        self.max_admit = max_admit or engine.max_batch
+        self.name = name
+        self._queue: deque[_Req] = deque()
+        self._cv = threading.Condition()
+        self._free = list(range(engine.max_batch))
+        heapq.heapify(self._free)
+        self._active: dict[int, _Req] = {}
+        self._stop = False
+        self._error: BaseException | None = None
+        self.steps = 0
+        self.completed = 0
+        self._thread = threading.Thread(target=self._run, name=f"{name}-batcher", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------ client side
+    def submit(self, prompt: list[int]) -> Future:
+        fut: Future = Future()
+        eos, T = self.engine.cfg.eos_token_id, self.engine.max_length
+        p = list(prompt) if len(prompt) else [eos]
+        if len(p) >= T:  # nothing to generate (generate() pass-through semantics)
+            fut.set_result(p)
+            return fut
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("batcher stopped")
+            if self._error is not None:
+                raise RuntimeError("batcher failed") from self._error
+            self._queue.append(_Req(p, fut))
+            self._cv.notify()
+        return fut
+
+    def generate(self, prompts: list[list[int]], timeout: float | None = None) -> list[list[int]]:
+        futs = [self.submit(p) for p in prompts]
+        return [f.result(timeout) for f in futs]
+
+    def stop(self, timeout: float = 10.0):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._thread.join(timeout)
+
+    @property
+    def active(self) -> int:
+        return len(self._active)
+
+    # ------------------------------------------------------------------ scheduler thread
+    def _run(self):
+        dev = getattr(self.engine, "device", None)
+        if dev is not None and getattr(dev, "type", None) == "cuda":
+            torch.cuda.set_device(dev)
+        try:
+            with torch.no_grad():
+                self._loop()
+        except BaseException as e:  # fail every waiter loudly instead of hanging them
+            with self._cv:
+                self._error = e
+                waiters = list(self._active.values()) + list(self._queue)
+                self._active.clear()
+                self._queue.clear()
+            for r in waiters:
+                if not r.future.done():
+                    r.future.set_exception(e)
+
+    def _loop(self):
+        eng = self.engine
+        while True:
+            with self._cv:
+                while not self._stop and not self._queue and not self._active:
+                    self._cv.wait()
+                if self._stop:
+                    waiters = list(self._queue) + list(self._active.values())
+                    self._queue.clear()
+                    self._active.clear()
+                    for r in waiters:
+                        if not r.future.done():
+                            r.future.set_exception(RuntimeError("batcher stopped"))
+                    return
+                admits: list[tuple[int, _Req]] = []
+                while self._queue and self._free and len(admits) < self.max_admit:
+                    admits.append((heapq.heappop(self._free), self._queue.popleft()))
+            if admits:
+                eng.admit([r.prompt for _, r in admits], [s for s, _ in admits], self.penalty)
+                for s, r in admits:
+                    self._active[s] = r
+                    METRICS.observe(f"{self.name}_queue_ms", (time.perf_counter() - r.t_submit) * 1e3)
+            B = min(_bucket(max(self._active) + 1), eng.max_batch)
+            eng.decode(B, self.chunk, self.penalty)
+            self.steps += self.chunk
+            flags = eng.finished_flags(B)
+            done = [s for s in self._active if flags[s]]
+            if not done:
+                continue
+            outs = eng.collect(done)
+            now = time.perf_counter()
+            with self._cv:
+                for s, out in zip(done, outs):
+                    r = self._active.pop(s)
+                    heapq.heappush(self._free, s)
+                    self.completed += 1
+                    METRICS.observe(f"{self.name}_request_ms", (now - r.t_submit) * 1e3)
+                    METRICS.inc(f"{self.name}_tokens", len(out) - len(r.prompt))
+                    r.future.set_result(out)
+            METRICS.set(f"{self.name}_active", len(self._active))

@@ -280,9 +280,11 @@ static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int
     return hipGetLastError();
 }
 
-// Tile selection.  Decode GEMMs (M = live batch <= 256) are latency-bound: prefer the tile count
-// that covers the 256 CUs; prefill / encoder / LM-head GEMMs take 128-wide tiles (less operand
-// re-reading per MFMA).
+// Tile selection, fit to the graph-replay sweep in profiles/r1_gemm_tile_sweep.jsonl (M = 256 and
+// 1024, GPT-2 shapes): a 2-deep LDS ring beats 3-4 deep at every shape (two workgroups per CU hide
+// the load latency better than one deeper ring), 64x64 wins wherever it yields < ~512
+// 128x128-tiles, and only grids with >= 512 128x128-tiles (LM head, prefill) amortise the bigger
+// tile's operand reuse.  The 8-wave variants never won and stay tuning-only.
 static int g_force_tile = -1;  // tuning override (dlms_gemm_force_tile), -1 = heuristic
 
 template <int EPI>
@@ -325,10 +327,8 @@ static hipError_t launch_gemm_epi(const bf16_t* A, int lda, const bf16_t* W, int
     }
     if (M <= 32) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     const long t128x128 = (long)((M + 127) / 128) * (N / 128) * split;
-    const long t128x64 = (long)((M + 127) / 128) * (N / 64) * split;
-    if (N % 128 == 0 && t128x128 >= 256) return launch_gemm_cfg<128, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    if (t128x64 >= 256) return launch_gemm_cfg<128, 64, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (N % 128 == 0 && t128x128 >= 512) return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    return launch_gemm_cfg<64, 64, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
 }
 
 extern "C" void dlms_gemm_force_tile(int id) { g_force_tile = id; }

@@ -4,11 +4,13 @@ Reference behaviour (``tutoring_server.py:15-49``): wrap the query in a fixed pr
 ``generate(max_length=150, repetition_penalty=1.2)`` (greedy), return the decoded sequence -- prompt
 included -- with ``success=True``; listen on ``[::]:50054`` with 10 worker threads.
 
-Here concurrent queries are batched: a batcher thread collects requests for up to
-``batch_window_ms`` (or until ``max_batch``) and runs them as ONE batched prefill + hipGraph decode
-on the GPU (``engine/gpt2_engine.py``); on a CPU-only host the same batching runs on the torch
-reference engine (BASELINE config 1).  Per-request latency, batch sizes and tokens/s land in the
-metrics registry.
+Here concurrent queries are batched.  On the GPU engine the default is continuous batching
+(``engine/scheduler.py``): a query is prefilled into a free KV-cache slot of the running batch as
+soon as it arrives and leaves at its own EOS/max_length, every live query advancing in
+hipGraph-replayed decode chunks.  The window batcher (``--batching window``, and the only mode of
+the CPU torch reference engine, BASELINE config 1) collects requests for up to
+``batch_window_ms`` (or until ``max_batch``) and runs them as one batched ``generate``.
+Per-request latency, batch sizes and tokens/s land in the metrics registry.
 """
 from __future__ import annotations
 
@@ -146,10 +148,20 @@ def make_engine(model: str, device: str, max_batch: int, max_length: int, weight
 class TutoringServer:
     def __init__(self, engine, port: int = 50054, host: str = "[::]", max_batch: int = 64, window_ms: float = 2.0,
                  max_length: int = 150, repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None,
-                 workers: int = 64):
+                 workers: int = 64, batching: str = "auto", chunk: int = 8):
         self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
         self.tok = tokenizer or GPT2BPE(eos_token_id=getattr(getattr(engine, "cfg", None), "eos_token_id", 50256))
-        self.batcher = Batcher(engine, self.gen, max_batch=max_batch, window_ms=window_ms)
+        if batching == "auto":
+            batching = "continuous" if hasattr(engine, "admit") else "window"
+        if batching == "continuous":
+            from ..engine.scheduler import ContinuousBatcher
+
+            if engine.max_length != max_length:
+                raise ValueError("continuous batching: engine max_length differs from the server's")
+            self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
+        else:
+            self.batcher = Batcher(engine, self.gen, max_batch=max_batch, window_ms=window_ms)
+        self.batching = batching
         self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
                                   options=[("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
                                            ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)])
@@ -181,6 +193,8 @@ def main(argv=None):
     ap.add_argument("--window-ms", type=float, default=2.0)
     ap.add_argument("--max-length", type=int, default=150)
     ap.add_argument("--repetition-penalty", type=float, default=1.2)
+    ap.add_argument("--batching", choices=("auto", "continuous", "window"), default="auto")
+    ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     args = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
@@ -188,7 +202,7 @@ def main(argv=None):
     eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights)
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
-                         args.repetition_penalty, tokenizer=tok).start()
+                         args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk).start()
     print(f"Tutoring Server started on port {srv.port}", flush=True)
     done = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: done.set())

@@ -74,3 +74,37 @@ def test_graph_replay_equals_eager():
     a = HipGPT2Engine(cfg, w, max_batch=8, max_length=80, use_graph=True).generate(prompts)
     b = HipGPT2Engine(cfg, w, max_batch=8, max_length=80, use_graph=False).generate(prompts)
     assert a == b
+
+
+def test_continuous_batching_matches_static():
+    """Requests admitted into free slots of a running batch (8 slots, 14 staggered requests)
+    produce what a static batch of each request alone produces."""
+    import time
+
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+    from distributed_lms_raft_llm_amd.engine.scheduler import ContinuousBatcher
+
+    cfg, w = _setup("gpt2")
+    T = 64
+    prompts = _prompts(cfg, [3, 30, 12, 1, 25, 7, 40, 16, 2, 33, 9, 21, 5, 63], seed=3)
+    eng = HipGPT2Engine(cfg, w, max_batch=8, max_length=T)
+    cb = ContinuousBatcher(eng, repetition_penalty=1.2, chunk=4)
+    try:
+        futs = []
+        for i, p in enumerate(prompts):
+            futs.append(cb.submit(p))
+            if i % 4 == 3:
+                time.sleep(0.02)
+        got = [f.result(120) for f in futs]
+    finally:
+        cb.stop()
+    solo = HipGPT2Engine(cfg, w, max_batch=1, max_length=T)
+    for g_, p in zip(got, prompts):
+        r_ = solo.generate([p], repetition_penalty=1.2)[0]
+        assert g_[: len(p)] == p and len(g_) <= T
+        n = min(len(g_), len(r_))
+        if n > len(p):
+            assert g_[len(p)] == r_[len(p)]
+            agree = sum(int(a == b) for a, b in zip(g_[len(p): n], r_[len(p): n]))
+            assert agree >= 0.5 * (n - len(p)), (g_, r_)
+    assert cb.completed == len(prompts)

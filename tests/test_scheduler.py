@@ -1,0 +1,138 @@
+"""Continuous-batching scheduler (engine/scheduler.py) on a CPU fake engine that follows the slot
+protocol: admission into free slots while others run, slot reuse, per-request outputs identical
+to running each request alone, pass-through of degenerate prompts, loud failure propagation."""
+import threading
+import time
+from types import SimpleNamespace
+
+import pytest
+
+from distributed_lms_raft_llm_amd.engine.scheduler import ContinuousBatcher
+
+V, EOS = 97, 96
+
+
+def next_token(seq):
+    return (sum(seq) * 31 + len(seq) * 7) % V
+
+
+def solo(prompt, T):
+    seq = list(prompt)
+    while len(seq) < T:
+        t = next_token(seq)
+        seq.append(t)
+        if t == EOS:
+            break
+    return seq
+
+
+class FakeSlotEngine:
+    def __init__(self, max_batch=4, max_length=40):
+        self.max_batch, self.max_length = max_batch, max_length
+        self.cfg = SimpleNamespace(eos_token_id=EOS)
+        self.seqs = [[EOS] for _ in range(max_batch)]
+        self.fin = [1] * max_batch
+        self.lock = threading.Lock()
+        self.admitted_while_busy = 0
+        self.buckets = []
+        self.fail_after = None
+        self.stop_at_eos = True
+
+    def _step(self, s):
+        if self.fin[s]:
+            return
+        t = next_token(self.seqs[s])
+        self.seqs[s].append(t)
+        if (t == EOS and self.stop_at_eos) or len(self.seqs[s]) >= self.max_length:
+            self.fin[s] = 1
+
+    def admit(self, prompts, slots, penalty):
+        assert len(set(slots)) == len(slots)
+        if any(not f for f in self.fin):
+            self.admitted_while_busy += 1
+        for p, s in zip(prompts, slots):
+            assert self.fin[s], "admitted into a live slot"
+            self.seqs[s] = list(p)
+            self.fin[s] = 0
+            self._step(s)  # prefill emits the first token
+
+    def decode(self, B, steps, penalty):
+        self.buckets.append(B)
+        if self.fail_after is not None:
+            self.fail_after -= 1
+            if self.fail_after < 0:
+                raise RuntimeError("device lost")
+        assert not any(not self.fin[s] for s in range(B, self.max_batch)), "live slot outside bucket"
+        for _ in range(steps):
+            for s in range(B):
+                self._step(s)
+        time.sleep(0.001)
+
+    def finished_flags(self, B):
+        return self.fin[:B]
+
+    def collect(self, slots):
+        return [list(self.seqs[s]) for s in slots]
+
+
+def _prompts(n, seed=0):
+    import random
+
+    r = random.Random(seed)
+    return [[r.randrange(0, V - 1) for _ in range(r.randrange(1, 12))] for _ in range(n)]
+
+
+def test_outputs_match_solo_runs_with_staggered_arrivals():
+    eng = FakeSlotEngine(max_batch=4, max_length=40)
+    cb = ContinuousBatcher(eng, chunk=3)
+    try:
+        prompts = _prompts(23)
+        futs = []
+        for i, p in enumerate(prompts):
+            futs.append(cb.submit(p))
+            if i % 5 == 0:
+                time.sleep(0.005)
+        outs = [f.result(10) for f in futs]
+    finally:
+        cb.stop()
+    assert outs == [solo(p, 40) for p in prompts]
+    assert cb.completed == 23
+    assert eng.admitted_while_busy > 0  # requests joined a running batch
+    assert max(eng.buckets) <= 4
+
+
+def test_passthrough_and_empty_prompt():
+    eng = FakeSlotEngine(max_batch=2, max_length=10)
+    cb = ContinuousBatcher(eng)
+    try:
+        long = list(range(12))
+        assert cb.submit(long).result(5) == long
+        assert cb.submit([]).result(5) == solo([EOS], 10)
+    finally:
+        cb.stop()
+
+
+def test_engine_failure_fails_waiters_and_rejects_new():
+    eng = FakeSlotEngine(max_batch=2, max_length=400)
+    eng.fail_after = 1
+    cb = ContinuousBatcher(eng, chunk=1)
+    f = cb.submit([1, 2, 3])
+    with pytest.raises(RuntimeError, match="device lost"):
+        f.result(5)
+    time.sleep(0.05)
+    with pytest.raises(RuntimeError):
+        cb.submit([1])
+    cb.stop()
+
+
+def test_stop_cancels_pending():
+    eng = FakeSlotEngine(max_batch=1, max_length=10 ** 6)
+    eng.stop_at_eos = False  # neither request can finish before stop()
+    cb = ContinuousBatcher(eng, chunk=1)
+    f1 = cb.submit([1])
+    f2 = cb.submit([2])
+    time.sleep(0.02)
+    cb.stop()
+    for f in (f1, f2):
+        with pytest.raises(RuntimeError):
+            f.result(5)
