@@ -168,3 +168,59 @@ class TorchTPGPT2:
             h = self.forward(torch.tensor([t], device=self.device),
                              torch.tensor([len(seq) - 1], device=self.device), cache)
         return seq
+
+
+class TorchSlotEngine:
+    """The continuous-batching slot protocol (``engine/scheduler.py``) on ``TorchTPGPT2``: any
+    device/backend, TP over ``group`` or unsharded.  Every rank of a TP group must receive the
+    same admit/decode calls (``engine/tp_serving.py`` mirrors them); the per-slot token state is
+    identical on all ranks because the vocab-parallel argmax is all-gathered.  Sequences run one
+    after another inside a step (no batching) -- this is the executable specification and the
+    CPU serving path, the HIP engine is the fast one."""
+
+    def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor], group=None, max_batch: int = 8,
+                 max_length: int = 150, device="cpu"):
+        self.m = TorchTPGPT2(cfg, weights, group=group, device=device)
+        self.cfg, self.max_batch, self.max_length = cfg, max_batch, max_length
+        self.device = torch.device(device)
+        eos = cfg.eos_token_id
+        self.seqs = [[eos] for _ in range(max_batch)]
+        self.fin = [1] * max_batch
+        self.seen: list[set] = [set() for _ in range(max_batch)]
+        self.caches: list = [None] * max_batch
+
+    def _emit(self, s: int, hidden_last: torch.Tensor, penalty: float):
+        t = self.m.next_token(hidden_last, self.seen[s], penalty)
+        self.seqs[s].append(t)
+        self.seen[s].add(t)
+        if t == self.cfg.eos_token_id or len(self.seqs[s]) >= self.max_length:
+            self.fin[s] = 1
+            self.caches[s] = None
+
+    @torch.no_grad()
+    def admit(self, prompts: list[list[int]], slots: list[int], repetition_penalty: float = 1.2):
+        for p, s in zip(prompts, slots):
+            if not (0 <= s < self.max_batch) or not self.fin[s]:
+                raise ValueError(f"slot {s} is not free")
+            self.seqs[s], self.seen[s], self.fin[s] = list(p), set(p), 0
+            self.caches[s] = self.m.new_cache(self.max_length)
+            h = self.m.forward(torch.tensor(p, device=self.device), torch.arange(len(p), device=self.device),
+                               self.caches[s])
+            self._emit(s, h[-1], repetition_penalty)
+
+    @torch.no_grad()
+    def decode(self, B: int, steps: int, repetition_penalty: float = 1.2):
+        for _ in range(steps):
+            for s in range(B):
+                if self.fin[s]:
+                    continue
+                n = len(self.seqs[s])
+                h = self.m.forward(torch.tensor([self.seqs[s][-1]], device=self.device),
+                                   torch.tensor([n - 1], device=self.device), self.caches[s])
+                self._emit(s, h[-1], repetition_penalty)
+
+    def finished_flags(self, B: int) -> list[int]:
+        return list(self.fin[:B])
+
+    def collect(self, slots: list[int]) -> list[list[int]]:
+        return [list(self.seqs[s]) for s in slots]

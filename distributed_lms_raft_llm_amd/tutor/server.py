@@ -132,6 +132,8 @@ class TutoringServicer:
 
 def make_engine(model: str, device: str, max_batch: int, max_length: int, weights: str | None = None, seed: int = 0,
                 tp_group=None):
+    """GPU: the HIP engine (TP over ``tp_group`` when given).  CPU: the torch reference engine, or
+    the sharded torch slot engine when a (gloo) TP group is given."""
     cfg = gpt2_config(model)
     w = load_safetensors_weights(weights) if weights else init_gpt2_weights(cfg, seed=seed)
     if device == "auto":
@@ -140,6 +142,10 @@ def make_engine(model: str, device: str, max_batch: int, max_length: int, weight
         from ..engine.gpt2_engine import HipGPT2Engine
 
         return HipGPT2Engine(cfg, w, device=device, max_batch=max_batch, max_length=max_length, tp_group=tp_group)
+    if tp_group is not None:
+        from ..parallel.tp import TorchSlotEngine
+
+        return TorchSlotEngine(cfg, w, group=tp_group, max_batch=max_batch, max_length=max_length)
     from ..engine.gpt2_engine import TorchGPT2Engine
 
     return TorchGPT2Engine(cfg, w, max_length=max_length)
@@ -193,13 +199,41 @@ def main(argv=None):
     ap.add_argument("--window-ms", type=float, default=2.0)
     ap.add_argument("--max-length", type=int, default=150)
     ap.add_argument("--repetition-penalty", type=float, default=1.2)
+    ap.add_argument("--tp", type=int, default=0, help="tensor-parallel degree under torchrun (default: world)")
     ap.add_argument("--batching", choices=("auto", "continuous", "window"), default="auto")
     ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     args = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    tp_group = proxy = None
+    if world > 1:  # torchrun: TP groups of --tp consecutive ranks, one front end (port + group) each
+        import torch.distributed as dist
+
+        from ..engine.tp_serving import TPEngineProxy, serve_follower
+        from ..parallel.tp import init_distributed, tp_groups
+
+        rank, world, local = init_distributed("nccl" if args.device != "cpu" and torch.cuda.is_available()
+                                              else "gloo")
+        tp = args.tp or world
+        tp_group, dp_idx, _ = tp_groups(tp)
+        ctrl = None
+        for g in range(world // tp):  # every rank creates every group, keeps its own
+            grp = dist.new_group(list(range(g * tp, (g + 1) * tp)), backend="gloo")
+            if g == dp_idx:
+                ctrl = grp
+        src = dp_idx * tp
+        device = f"cuda:{local}" if args.device != "cpu" and torch.cuda.is_available() else "cpu"
+        eng = make_engine(args.model, device, args.max_batch, args.max_length, args.weights, tp_group=tp_group)
+        if rank != src:
+            n = serve_follower(eng, ctrl, src)
+            log.info("TP follower rank %d done after %d commands", rank, n)
+            return
+        proxy = eng = TPEngineProxy(eng, ctrl, src)
+        args.port += dp_idx
+    else:
+        eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights)
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
                          args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk).start()
@@ -209,6 +243,8 @@ def main(argv=None):
     signal.signal(signal.SIGINT, lambda *a: done.set())
     done.wait()
     srv.stop()
+    if proxy is not None:
+        proxy.close()
 
 
 if __name__ == "__main__":
