@@ -28,6 +28,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ..utils.metrics import METRICS
+from ..utils.trace import TRACER, roctx_range
 from .gpt2_engine import _bucket
 
 
@@ -125,14 +126,22 @@ class ContinuousBatcher:
                 while self._queue and self._free and len(admits) < self.max_admit:
                     admits.append((heapq.heappop(self._free), self._queue.popleft()))
             if admits:
-                eng.admit([r.prompt for _, r in admits], [s for s, _ in admits], self.penalty)
+                ta = time.perf_counter()
+                with roctx_range("prefill"):
+                    eng.admit([r.prompt for _, r in admits], [s for s, _ in admits], self.penalty)
+                TRACER.complete("tutor.admit", ta, cat="tutor", n=len(admits),
+                                tokens=sum(len(r.prompt) for _, r in admits))
                 for s, r in admits:
                     self._active[s] = r
                     METRICS.observe(f"{self.name}_queue_ms", (time.perf_counter() - r.t_submit) * 1e3)
             B = min(_bucket(max(self._active) + 1), eng.max_batch)
-            eng.decode(B, self.chunk, self.penalty)
+            td = time.perf_counter()
+            with roctx_range("decode_chunk"):
+                eng.decode(B, self.chunk, self.penalty)
+                flags = eng.finished_flags(B)  # the sync point of the chunk
             self.steps += self.chunk
-            flags = eng.finished_flags(B)
+            TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
+                            steps=self.chunk)
             done = [s for s in self._active if flags[s]]
             if not done:
                 continue

@@ -25,6 +25,7 @@ from ..raft.core import RaftConfig
 from ..raft.node import RaftNode
 from ..raft.storage import FileStorage
 from ..raft.transport import GrpcTransport, RaftServicer, snapshot_handler
+from ..utils.debug_rpc import debug_handler
 from .service import FileTransferServicer, LMSServicer, TutoringClient
 from .state import LMSState
 
@@ -65,11 +66,17 @@ class LMSServer:
         wire.register(self.server, "LMS", self.lms)
         wire.register(self.server, "RaftService", self.raft_servicer)
         wire.register(self.server, "FileTransferService", FileTransferServicer(self.state))
-        self.server.add_generic_rpc_handlers((snapshot_handler(self.node),))
+        self.server.add_generic_rpc_handlers((snapshot_handler(self.node),
+                                              debug_handler(health=self._health, status=self.node.status)))
         bound = self.server.add_insecure_port(f"{host}:{port}")
         if bound == 0:
             raise RuntimeError(f"could not bind {host}:{port}")
         self.port = bound
+
+    def _health(self) -> dict:
+        st = self.node.status()
+        return {"node": self.id, "role": st["role"], "leader": st["leader"], "term": st["term"],
+                "ok": st["leader"] is not None}
 
     def start(self):
         self.server.start()

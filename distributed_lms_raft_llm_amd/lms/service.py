@@ -19,6 +19,7 @@ from __future__ import annotations
 import base64
 import hashlib
 import logging
+import threading
 import time
 import uuid
 
@@ -27,6 +28,7 @@ import grpc
 from .. import wire
 from ..raft.core import NotLeader
 from ..utils.metrics import METRICS
+from ..utils.trace import TRACER
 from ..wire import pb
 from . import commands
 from .pdf import extract_text
@@ -58,17 +60,59 @@ MSG_TUTOR_UNAVAILABLE = "The tutoring service is unavailable. Please retry later
 
 
 class TutoringClient:
-    def __init__(self, address: str, timeout: float = 120.0):
-        self.address = address
+    """Client of the tutoring tier.  ``address`` may list several tutoring replicas (one per GPU or
+    TP group, comma-separated): a query goes to the replica with the fewest queries in flight and
+    fails over to the next one when a replica is unreachable (UNAVAILABLE / connection errors
+    mark it down for ``down_s``), so a dead tutoring process costs one retry, not an outage.
+    The reference has one module-level channel to a hard-coded address (``lms_server.py:39-40``)."""
+
+    RETRY_CODES = (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.CANCELLED)
+
+    def __init__(self, address, timeout: float = 120.0, down_s: float = 2.0):
+        addrs = address.split(",") if isinstance(address, str) else list(address)
+        self.addresses = [a.strip() for a in addrs if a.strip()]
+        if not self.addresses:
+            raise ValueError("no tutoring address")
+        self.address = self.addresses[0]
         self.timeout = timeout
-        self._channel = wire.channel(address)
-        self._stub = wire.Stub("Tutoring", self._channel)
+        self.down_s = down_s
+        self._channels = [wire.channel(a) for a in self.addresses]
+        self._stubs = [wire.Stub("Tutoring", c) for c in self._channels]
+        self._inflight = [0] * len(self.addresses)
+        self._down_until = [0.0] * len(self.addresses)
+        self._lock = threading.Lock()
+
+    def _order(self) -> list[int]:
+        now = time.monotonic()
+        with self._lock:
+            up = [i for i in range(len(self.addresses)) if self._down_until[i] <= now]
+            down = [i for i in range(len(self.addresses)) if self._down_until[i] > now]
+            up.sort(key=lambda i: self._inflight[i])
+        return up + down  # down replicas last: still tried if nothing else answers
 
     def ask(self, token: str, query: str) -> pb.QueryResponse:
-        return self._stub.GetLLMAnswer(pb.QueryRequest(token=token, query=query), timeout=self.timeout)
+        last = None
+        for i in self._order():
+            with self._lock:
+                self._inflight[i] += 1
+            try:
+                return self._stubs[i].GetLLMAnswer(pb.QueryRequest(token=token, query=query), timeout=self.timeout)
+            except grpc.RpcError as e:
+                last = e
+                if e.code() not in self.RETRY_CODES:
+                    raise
+                METRICS.inc("tutor_failover_total")
+                log.warning("tutoring replica %s unavailable, failing over", self.addresses[i])
+                with self._lock:
+                    self._down_until[i] = time.monotonic() + self.down_s
+            finally:
+                with self._lock:
+                    self._inflight[i] -= 1
+        raise last
 
     def close(self):
-        self._channel.close()
+        for c in self._channels:
+            c.close()
 
 
 class LMSServicer:
@@ -318,17 +362,21 @@ class LMSServicer:
             tg = time.perf_counter()
             relevant, sim = self.gate.check(request.query, assignment_text)
             METRICS.observe("gate_ms", (time.perf_counter() - tg) * 1e3)
+            TRACER.complete("lms.gate", tg, cat="lms", similarity=round(float(sim), 4), relevant=bool(relevant))
             METRICS.observe("gate_similarity", sim)
             if not relevant:
                 METRICS.inc("gate_rejected_total")
                 return pb.QueryResponse(success=True, response=MSG_LLM_IRRELEVANT)
         if self.tutor is None:
             return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        tt = time.perf_counter()
         try:
             resp = self.tutor.ask(request.token, request.query)
         except grpc.RpcError as e:
             log.warning("tutoring call failed: %s", e.code())
             return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        TRACER.complete("lms.tutor_call", tt, cat="lms")
+        TRACER.complete("lms.GetLLMAnswer", t0, cat="lms", user=user)
         METRICS.observe("llm_answer_ms", (time.perf_counter() - t0) * 1e3)
         return resp
 

@@ -19,6 +19,8 @@ import threading
 import time
 from concurrent.futures import Future
 
+from ..utils.metrics import METRICS
+from ..utils.trace import TRACER
 from .core import LEADER, REQUESTS, NotLeader, RaftConfig, RaftCore
 
 log = logging.getLogger("dlms.raft")
@@ -44,6 +46,7 @@ class RaftNode:
         self._threads: list[threading.Thread] = []
         self.applied_index = self.core.last_applied
         self._applied_cv = threading.Condition()
+        self._seen = (self.core.role, self.core.current_term, self.core.leader_id)
         snap = storage.snapshot_data()
         if snap:
             state_machine.restore(snap)
@@ -82,12 +85,30 @@ class RaftNode:
         return reply
 
     def _collect(self):
-        """Move committed entries to the apply queue (caller holds the lock)."""
+        """Move committed entries to the apply queue and record role/term/leader transitions
+        (caller holds the lock)."""
         if self.core.pending_restore is not None:
             self._apply_q.put(("restore", self.core.last_applied, self.core.pending_restore))
             self.core.pending_restore = None
-        for idx, e in self.core.take_committed():
+            TRACER.instant("raft.install_snapshot", cat="raft", node=self.id, index=self.core.last_applied)
+        committed = self.core.take_committed()
+        for idx, e in committed:
             self._apply_q.put(("entry", idx, e))
+        if committed:
+            TRACER.instant("raft.commit", cat="raft", node=self.id, first=committed[0][0], last=committed[-1][0])
+        cur = (self.core.role, self.core.current_term, self.core.leader_id)
+        if cur != self._seen:
+            role, term, leader = cur
+            if term != self._seen[1]:
+                METRICS.set(f"raft_term_n{self.id}", term)
+            if role != self._seen[0]:
+                if role == LEADER:
+                    METRICS.inc("raft_leaderships_won")
+                    log.info("node %d became leader for term %d", self.id, term)
+                elif role == "candidate":
+                    METRICS.inc("raft_elections_started")
+            TRACER.instant("raft.transition", cat="raft", node=self.id, role=role, term=term, leader=leader)
+            self._seen = cur
 
     def _tick_loop(self):
         while not self._stop.is_set():

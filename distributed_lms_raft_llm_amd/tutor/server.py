@@ -31,6 +31,7 @@ from .. import wire
 from ..models.config import GenerationConfig, gpt2_config
 from ..models.gpt2 import init_gpt2_weights, load_safetensors_weights
 from ..tokenizer import GPT2BPE
+from ..utils.debug_rpc import debug_handler
 from ..utils.metrics import METRICS
 from ..wire import pb
 
@@ -172,9 +173,21 @@ class TutoringServer:
                                   options=[("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
                                            ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)])
         wire.register(self.server, "Tutoring", TutoringServicer(self.batcher, self.tok, max_length))
+        self.engine = engine
+        self.server.add_generic_rpc_handlers((debug_handler(health=self._health),))
         self.port = self.server.add_insecure_port(f"{host}:{port}")
         if self.port == 0:
             raise RuntimeError(f"could not bind {host}:{port}")
+
+    def _health(self) -> dict:
+        b = self.batcher
+        out = {"batching": self.batching, "engine": type(getattr(self.engine, "engine", self.engine)).__name__,
+               "max_length": self.gen.max_length}
+        if self.batching == "continuous":
+            out.update(active=b.active, completed=b.completed, ok=b._error is None and b._thread.is_alive())
+        else:
+            out.update(queued=b.q.qsize(), ok=b._t.is_alive())
+        return out
 
     def start(self):
         self.server.start()
