@@ -83,8 +83,8 @@ def _bucket(n: int) -> int:
 
 class HipGPT2Engine:
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
-                 max_batch: int = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
-                 check_every: int = 16):
+                 max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
+                 check_every: int = 16, max_batch_cap: int = 4096):
         if not torch.cuda.is_available():
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
@@ -101,10 +101,15 @@ class HipGPT2Engine:
             self.w = weights
         else:
             self.w = prepare_gpt2_weights(cfg, weights, self.device, self.tp_rank, self.tp_size)
-        self.max_batch = max_batch
-        self.max_length = max_length
         if max_length > cfg.n_positions:
             raise ValueError("max_length exceeds n_positions")
+        if not max_batch or max_batch == "auto":  # size the slot pool from free HBM (engine/memory.py)
+            from .memory import plan_max_batch
+
+            max_batch = plan_max_batch(cfg, max_length, self.tp_size, weights_resident=True, cap=max_batch_cap,
+                                       device=self.device)
+        self.max_batch = int(max_batch)
+        self.max_length = max_length
         self.use_graph = use_graph
         self.check_every = check_every
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}

@@ -25,6 +25,7 @@ from ..raft.core import RaftConfig
 from ..raft.node import RaftNode
 from ..raft.storage import FileStorage
 from ..raft.transport import GrpcTransport, RaftServicer, snapshot_handler
+from ..utils.config import parse_with_config
 from ..utils.debug_rpc import debug_handler
 from .service import FileTransferServicer, LMSServicer, TutoringClient
 from .state import LMSState
@@ -98,10 +99,24 @@ class LMSServer:
         self.transport.blocked.update(peers)
 
 
+def cluster_from_args(args, conf: dict) -> tuple[dict[int, str], int, str | None]:
+    """(peers by real id, listen port, advertised address) from the positional form
+    ``<id> <port> <peers...>`` or from a config file's ``servers`` map."""
+    servers = {int(k): str(v) for k, v in (conf.get("servers") or {}).items()}
+    if servers and not args.peers:
+        if args.id not in servers:
+            raise SystemExit(f"server id {args.id} not in the config's servers {sorted(servers)}")
+        port = args.port or int(servers[args.id].rsplit(":", 1)[1])
+        return {i: a for i, a in servers.items() if i != args.id}, port, args.advertise or servers[args.id]
+    if args.port is None:
+        raise SystemExit("port required (or --config with a servers map)")
+    return dict(zip(peer_ids(args.id, len(args.peers)), args.peers)), args.port, args.advertise
+
+
 def build_arg_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="Raft-replicated LMS server (MI355X-native framework)")
     ap.add_argument("id", type=int, help="this server's id (1..N)")
-    ap.add_argument("port", type=int)
+    ap.add_argument("port", type=int, nargs="?", default=None, help="listen port (default: from --config servers)")
     ap.add_argument("peers", nargs="*", help="addresses of the other servers, in server-id order")
     ap.add_argument("--host", default="[::]")
     ap.add_argument("--advertise", default=None, help="address other nodes/clients use for this server")
@@ -123,11 +138,11 @@ def build_arg_parser() -> argparse.ArgumentParser:
 
 
 def main(argv=None):
-    args = build_arg_parser().parse_args(argv)
+    args, conf = parse_with_config(build_arg_parser(), argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    ids = peer_ids(args.id, len(args.peers))
-    peers = dict(zip(ids, args.peers))
+    peers, port, advertise = cluster_from_args(args, conf)
+    args.port, args.advertise = port, advertise
     lo, hi = (float(x) for x in args.election_timeout.split(","))
     cfg = RaftConfig(election_timeout=(lo, hi), heartbeat_interval=args.heartbeat)
     gate = None

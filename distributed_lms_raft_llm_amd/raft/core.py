@@ -42,14 +42,16 @@ class VoteRequest:
     term: int
     last_log_index: int
     last_log_term: int
+    pre: bool = False  # Pre-Vote probe (Raft thesis §9.6): ``term`` is the term it WOULD start
 
 
 @dataclass
 class VoteResponse:
     src: int
     dst: int
-    term: int
+    term: int  # pre-vote granted: the probed term; otherwise the responder's current term
     granted: bool
+    pre: bool = False
 
 
 @dataclass
@@ -109,6 +111,10 @@ class RaftConfig:
     max_entries_per_append: int = 256
     max_bytes_per_append: int = 8 << 20
     check_quorum: bool = True
+    # Pre-Vote + leader stickiness: a node that was partitioned or restarted (and whose election
+    # timer fired) first asks whether it COULD win; nodes that heard from a live leader within
+    # the minimum election timeout refuse, so it cannot force a term bump on a healthy cluster.
+    pre_vote: bool = True
 
 
 @dataclass
@@ -150,6 +156,8 @@ class RaftCore:
         self.commit_index = snap_index
         self.last_applied = snap_index
         self.votes: set[int] = set()
+        self.prevotes: set[int] | None = None  # collecting pre-votes (role stays FOLLOWER)
+        self._leader_contact = -1e9  # last time a current leader reached us
         self.pending_restore: str | None = None  # snapshot data the state machine must load
         self.stats = Stats()
         self._deadline = 0.0
@@ -195,6 +203,7 @@ class RaftCore:
         self.role = FOLLOWER
         self.leader_id = leader
         self.votes.clear()
+        self.prevotes = None
         self._reset_election_timer(now)
 
     # ------------------------------------------------------------------ timers
@@ -213,8 +222,24 @@ class RaftCore:
                                        or p.next_index <= self.last_index()):
                     out.extend(self._replicate_to(pid, now))
         elif now >= self._deadline:
-            out.extend(self._start_election(now))
+            if self.cfg.pre_vote and self.role == FOLLOWER:
+                out.extend(self._start_pre_vote(now))
+            else:
+                out.extend(self._start_election(now))
         return out
+
+    def _start_pre_vote(self, now: float) -> list:
+        self.prevotes = {self.id}
+        self.leader_id = None
+        self._event("pre_vote")
+        self._reset_election_timer(now)
+        if len(self.prevotes) >= self.quorum:
+            return self._start_election(now)
+        li, lt = self.last_index(), self.last_term()
+        return [VoteRequest(self.id, pid, self.current_term + 1, li, lt, pre=True) for pid in self.peers]
+
+    def _in_leader_lease(self, now: float) -> bool:
+        return self.role == LEADER or now - self._leader_contact < self.cfg.election_timeout[0]
 
     def _quorum_recent(self, now: float) -> bool:
         window = self.cfg.election_timeout[1]
@@ -222,6 +247,7 @@ class RaftCore:
         return alive >= self.quorum
 
     def _start_election(self, now: float) -> list:
+        self.prevotes = None
         self.role = CANDIDATE
         self._set_term(self.current_term + 1, self.id)
         self.leader_id = None
@@ -308,9 +334,22 @@ class RaftCore:
     # ------------------------------------------------------------------ message handling
     def step(self, msg, now: float) -> list:
         term = msg.term
+        if isinstance(msg, VoteRequest) and msg.pre:
+            return [self._on_pre_vote_request(msg, now)]
+        if isinstance(msg, VoteResponse) and msg.pre and msg.granted:
+            return self._on_pre_vote_response(msg, now)  # carries the probed term: never adopt it
+        if isinstance(msg, VoteRequest) and self.cfg.check_quorum and term > self.current_term \
+                and self._in_leader_lease(now):
+            # leader stickiness: ignore (do not even adopt the term of) a disruptive candidate
+            return [VoteResponse(self.id, msg.src, self.current_term, False)]
         if term > self.current_term:
             leader = msg.src if isinstance(msg, (AppendRequest, SnapshotRequest)) else None
             self._become_follower(term, now, leader)
+        if isinstance(msg, (AppendRequest, SnapshotRequest)) and term == self.current_term:
+            self._leader_contact = now
+            self.prevotes = None
+        if isinstance(msg, VoteResponse) and msg.pre:
+            return []  # refused pre-vote (a higher term was adopted above)
         if isinstance(msg, VoteRequest):
             return [self._on_vote_request(msg, now)]
         if isinstance(msg, VoteResponse):
@@ -338,6 +377,21 @@ class RaftCore:
                 self._set_term(self.current_term, m.src)
             self._reset_election_timer(now)
         return VoteResponse(self.id, m.src, self.current_term, granted)
+
+    def _on_pre_vote_request(self, m: VoteRequest, now: float) -> VoteResponse:
+        """Grant iff a real vote at ``m.term`` could be granted and no live leader is known.
+        Changes no state: no term adoption, no vote recorded, no timer reset."""
+        granted = (m.term > self.current_term and not self._in_leader_lease(now)
+                   and self._log_up_to_date(m.last_log_index, m.last_log_term))
+        return VoteResponse(self.id, m.src, m.term if granted else self.current_term, granted, pre=True)
+
+    def _on_pre_vote_response(self, m: VoteResponse, now: float) -> list:
+        if self.prevotes is None or self.role != FOLLOWER or m.term != self.current_term + 1:
+            return []
+        self.prevotes.add(m.src)
+        if len(self.prevotes) >= self.quorum:
+            return self._start_election(now)
+        return []
 
     def _on_vote_response(self, m: VoteResponse, now: float) -> list:
         if self.role != CANDIDATE or m.term != self.current_term or not m.granted:

@@ -55,8 +55,11 @@ def to_proto(m):
     raise TypeError(type(m))
 
 
-def vote_request_from(p, dst: int) -> VoteRequest:
-    return VoteRequest(p.candidate.candidateID, dst, p.candidate.term, p.lastLogIndex, p.lastLogTerm)
+PREVOTE_HEADER = "x-dlms-prevote"  # lms.proto has no pre-vote flag: it rides in call metadata
+
+
+def vote_request_from(p, dst: int, pre: bool = False) -> VoteRequest:
+    return VoteRequest(p.candidate.candidateID, dst, p.candidate.term, p.lastLogIndex, p.lastLogTerm, pre=pre)
 
 
 def append_request_from(p, dst: int) -> AppendRequest:
@@ -71,7 +74,9 @@ class GrpcTransport:
         self.node = None
         self.rpc_timeout = rpc_timeout
         self.snapshot_timeout = snapshot_timeout
-        self._channels = {pid: wire.channel(addr) for pid, addr in peers.items()}
+        # fast reconnect: a restarted peer must hear heartbeats well within an election timeout
+        # (gRPC's default reconnect backoff grows to 120 s)
+        self._channels = {pid: wire.channel(addr, reconnect_ms=(50, 500)) for pid, addr in peers.items()}
         self._stubs = {pid: wire.Stub("RaftService", ch) for pid, ch in self._channels.items()}
         self._snap = {pid: ch.unary_unary(SNAPSHOT_METHOD) for pid, ch in self._channels.items()}
         self._pools = {pid: ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"raft-send-{pid}")
@@ -90,8 +95,9 @@ class GrpcTransport:
     def _send_sync(self, m):
         try:
             if isinstance(m, VoteRequest):
-                r = self._stubs[m.dst].RequestVote(to_proto(m), timeout=self.rpc_timeout)
-                resp = VoteResponse(m.dst, self.id, r.result.term, r.result.verdict)
+                md = ((PREVOTE_HEADER, "1"),) if m.pre else None
+                r = self._stubs[m.dst].RequestVote(to_proto(m), timeout=self.rpc_timeout, metadata=md)
+                resp = VoteResponse(m.dst, self.id, r.result.term, r.result.verdict, pre=m.pre)
             elif isinstance(m, AppendRequest):
                 r = self._stubs[m.dst].AppendEntries(to_proto(m), timeout=self.rpc_timeout)
                 resp = AppendResponse(m.dst, self.id, r.result.term, r.result.verdict, r.term)
@@ -132,7 +138,8 @@ class RaftServicer:
 
     def RequestVote(self, request, context):
         self._check(request.candidate.candidateID, context)
-        r = self.node.handle(vote_request_from(request, self.node.id))
+        pre = dict(context.invocation_metadata() or ()).get(PREVOTE_HEADER) == "1"
+        r = self.node.handle(vote_request_from(request, self.node.id, pre=pre))
         return to_proto(r)
 
     def AppendEntries(self, request, context):

@@ -31,6 +31,7 @@ from .. import wire
 from ..models.config import GenerationConfig, gpt2_config
 from ..models.gpt2 import init_gpt2_weights, load_safetensors_weights
 from ..tokenizer import GPT2BPE
+from ..utils.config import parse_with_config
 from ..utils.debug_rpc import debug_handler
 from ..utils.metrics import METRICS
 from ..wire import pb
@@ -146,7 +147,7 @@ def make_engine(model: str, device: str, max_batch: int, max_length: int, weight
     if tp_group is not None:
         from ..parallel.tp import TorchSlotEngine
 
-        return TorchSlotEngine(cfg, w, group=tp_group, max_batch=max_batch, max_length=max_length)
+        return TorchSlotEngine(cfg, w, group=tp_group, max_batch=max_batch or 8, max_length=max_length)
     from ..engine.gpt2_engine import TorchGPT2Engine
 
     return TorchGPT2Engine(cfg, w, max_length=max_length)
@@ -208,7 +209,8 @@ def main(argv=None):
     ap.add_argument("--vocab", default=None, help="GPT-2 vocab.json")
     ap.add_argument("--merges", default=None, help="GPT-2 merges.txt")
     ap.add_argument("--device", default=os.environ.get("DLMS_DEVICE", "auto"))
-    ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--max-batch", type=int, default=256,
+                    help="decode slots per engine; 0 = size from free HBM (engine/memory.py)")
     ap.add_argument("--window-ms", type=float, default=2.0)
     ap.add_argument("--max-length", type=int, default=150)
     ap.add_argument("--repetition-penalty", type=float, default=1.2)
@@ -216,7 +218,7 @@ def main(argv=None):
     ap.add_argument("--batching", choices=("auto", "continuous", "window"), default="auto")
     ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
-    args = ap.parse_args(argv)
+    args, _ = parse_with_config(ap, argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -247,6 +249,7 @@ def main(argv=None):
         args.port += dp_idx
     else:
         eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights)
+    args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
                          args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk).start()

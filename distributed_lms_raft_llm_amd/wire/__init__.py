@@ -65,6 +65,11 @@ def register(server: grpc.Server, service: str, servicer) -> None:
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(f"{PACKAGE}.{service}", handlers),))
 
 
-def channel(address: str, max_message: int = DEFAULT_MAX_MESSAGE) -> grpc.Channel:
-    return grpc.insecure_channel(address, options=[("grpc.max_send_message_length", max_message),
-                                                   ("grpc.max_receive_message_length", max_message)])
+def channel(address: str, max_message: int = DEFAULT_MAX_MESSAGE,
+            reconnect_ms: tuple[int, int] | None = None) -> grpc.Channel:
+    opts = [("grpc.max_send_message_length", max_message), ("grpc.max_receive_message_length", max_message)]
+    if reconnect_ms is not None:
+        opts += [("grpc.initial_reconnect_backoff_ms", reconnect_ms[0]),
+                 ("grpc.min_reconnect_backoff_ms", reconnect_ms[0]),
+                 ("grpc.max_reconnect_backoff_ms", reconnect_ms[1])]
+    return grpc.insecure_channel(address, options=opts)

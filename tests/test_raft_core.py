@@ -87,10 +87,10 @@ def test_minority_partition_cannot_commit_and_leader_steps_down():
     minority = [lid, [i for i in c.ids if i != lid][0]]
     majority = [i for i in c.ids if i not in minority]
     c.partition(minority, majority)
-    idx_before = c.nodes[lid].core.commit_index
-    c.nodes[lid].core.propose(cmd(7), c.now)
+    idx7 = c.nodes[lid].core.propose(cmd(7), c.now)
     c.run(1.0)
-    assert c.nodes[lid].core.commit_index == idx_before
+    # (entries replicated to a majority before the cut, e.g. the no-op, may still commit)
+    assert c.nodes[lid].core.commit_index < idx7
     # check-quorum: the isolated ex-leader stops claiming leadership
     assert c.nodes[lid].core.role != LEADER
     new = c.leader()
@@ -263,3 +263,46 @@ def test_randomized_faults_preserve_safety(seed):
     final = [user_cmds(c.committed_on(i)) for i in c.ids]
     assert all(f == final[0] for f in final)
     assert final[0][-1] == cmd(10_000)
+
+
+def test_pre_vote_rejoining_node_does_not_disrupt_leader():
+    """A follower cut off for many election timeouts keeps probing with pre-votes (its term never
+    moves), and when it rejoins the healthy leader keeps its term and leadership (Raft thesis
+    §9.6; without pre-vote the rejoining node's inflated term would force an election)."""
+    c = SimCluster(5, seed=11)
+    lid = c.wait_leader()
+    term = c.nodes[lid].core.current_term
+    victim = [i for i in c.ids if i != lid][0]
+    c.partition([victim], [i for i in c.ids if i != victim])
+    c.run(3.0)  # ~10-20 election timeouts on the victim
+    assert c.nodes[victim].core.current_term == term
+    assert c.nodes[victim].core.stats.elections_started == 0
+    c.heal()
+    c.run(1.0)
+    assert c.leader() == lid and c.nodes[lid].core.current_term == term
+    assert c.nodes[victim].core.leader_id == lid
+    c.check_safety()
+
+
+def test_pre_vote_is_side_effect_free_and_lease_refuses():
+    st = MemoryStorage()
+    core = RaftCore(1, [2, 3], st, now=0.0)
+    st.append([Entry(1, "a")])
+    st.save_meta(1, None)
+    core.current_term = 1
+    # no leader heard: a pre-vote for term 2 with an up-to-date log is granted, nothing persists
+    r = core.step(VoteRequest(2, 1, 2, last_log_index=1, last_log_term=1, pre=True), 1.0)[0]
+    assert r.granted and r.pre and r.term == 2
+    assert st.load_meta() == (1, None) and core.current_term == 1
+    # stale log: refused
+    r = core.step(VoteRequest(3, 1, 2, last_log_index=0, last_log_term=0, pre=True), 1.0)[0]
+    assert not r.granted
+    # after hearing from the leader of term 1, both pre-votes and real votes are refused in the lease
+    core.step(AppendRequest(3, 1, 1, 1, 1, [], 1), 2.0)
+    r = core.step(VoteRequest(2, 1, 2, last_log_index=1, last_log_term=1, pre=True), 2.05)[0]
+    assert not r.granted
+    r = core.step(VoteRequest(2, 1, 2, last_log_index=1, last_log_term=1), 2.05)[0]
+    assert not r.granted and core.current_term == 1
+    # once the lease lapsed, the real vote goes through
+    r = core.step(VoteRequest(2, 1, 2, last_log_index=1, last_log_term=1), 2.5)[0]
+    assert r.granted and core.current_term == 2

@@ -136,3 +136,20 @@ def test_stop_cancels_pending():
     for f in (f1, f2):
         with pytest.raises(RuntimeError):
             f.result(5)
+
+
+def test_kv_capacity_planner():
+    from distributed_lms_raft_llm_amd.engine.memory import GIB, plan_max_batch, slot_bytes
+    from distributed_lms_raft_llm_amd.models.config import gpt2_config
+
+    small = gpt2_config("gpt2")
+    # KV dominates: 12 layers * 2 * 12 heads * 150 * 64 * 2 B = 5.27 MiB per slot
+    assert 5.2 * 2**20 < slot_bytes(small, 150) < 5.5 * 2**20
+    assert plan_max_batch(small, 150, free_bytes=287 * GIB, cap=4096) == 4096
+    assert plan_max_batch(small, 150, free_bytes=287 * GIB, cap=10**9) == 49152
+    assert plan_max_batch(small, 150, free_bytes=8 * GIB) == 256  # 4 GiB reserve + prefill workspace
+    xl = gpt2_config("gpt2-xl")
+    # 25 heads over 8 ranks: rank 0 holds 4 heads -> the planner sizes for the biggest shard
+    assert slot_bytes(xl, 150, 8, 0) > slot_bytes(xl, 150, 8, 7)
+    with pytest.raises(MemoryError):
+        plan_max_batch(small, 150, free_bytes=1 * GIB)
