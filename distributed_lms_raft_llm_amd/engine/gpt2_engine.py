@@ -177,11 +177,12 @@ class HipGPT2Engine:
     def _split(self, M: int, N: int, K: int) -> int:
         """Split-K factor for a row-parallel projection (N = d): slice K until the grid covers the
         CUs (<= 1024 workgroups), keeping >= 3 K-steps per slice (>= 6 above M = 512, where the
-        extra partial slabs the add+LayerNorm re-reads start to cost).  Fit to the tile sweep
-        (profiles/r1_gemm_tile_sweep.jsonl): M=1024 c_proj split 4 10.4 us vs unsplit 17 us."""
+        extra partial slabs the add+LayerNorm re-reads start to cost).  Fit to the cold-weight tile
+        sweep (profiles/r1_gemm_tile_sweep_cold.jsonl): M=256 c_proj split 8 6.8 us vs unsplit
+        15.9 us; M=1024 split 4 12.9 us vs 17.1 us."""
         if self.tp_size > 1:
             return 1
-        bm = 32 if M <= 32 else 64
+        bm = 32 if M <= 64 else 64
         tiles = -(-M // bm) * (N // 64)
         ksteps = K // 64
         min_steps = 3 if M <= 512 else 6

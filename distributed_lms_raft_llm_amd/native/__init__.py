@@ -55,6 +55,7 @@ def lib():
             IP = ctypes.POINTER(ctypes.c_int)
             for name, args, res in [
                 ("dlms_bpe_create", [C, C], P), ("dlms_bpe_is_synthetic", [P], I), ("dlms_bpe_vocab_size", [P], I),
+                ("dlms_bpe_set_synthetic_words", [P, I], I),
                 ("dlms_bpe_encode", [P, C, I, IP, I], I), ("dlms_bpe_decode", [P, IP, I, C, I], I),
                 ("dlms_bpe_destroy", [P], None), ("dlms_wp_create", [C, I], P),
                 ("dlms_wp_encode", [P, C, I, I, I, IP, I], I), ("dlms_wp_special", [P, I], I),

@@ -8,6 +8,9 @@
 //     Loads vocab.json + merges.txt when given; without them (no network here) it runs on a
 //     synthetic vocabulary: the 256 byte tokens at GPT-2's ids 0..255, no merges, and ids >= 256
 //     decoded to deterministic pseudo-words so random-init model output is still printable text.
+//     Optional synthetic *word* mode (dlms_bpe_set_synthetic_words): every multi-byte pre-token
+//     gets one hashed id in [256, V-1) (byte fallback on a hash collision), so prompt lengths in
+//     tokens are close to real GPT-2 BPE's (~1 token per word) instead of 1 token per byte.
 //   * WordPiece: BERT's basic tokenizer (lower-case, accent-strip for Latin-1, split on whitespace
 //     and punctuation, CJK as single chars) + greedy longest-match-first sub-words with "##".
 //     Loads vocab.txt; without it a deterministic hashed vocabulary stands in.
@@ -19,6 +22,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <mutex>
 #include <vector>
 
 namespace {
@@ -135,6 +139,9 @@ struct BPE {
     std::unordered_map<std::string, std::vector<int>> cache;
     bool synthetic = false;
     int vocab_size = 50257;
+    int word_vocab = 0;                                  // synthetic word mode: model vocab size
+    std::unordered_map<int, std::string> word_of;        // hashed word id -> word bytes
+    std::mutex mu;                                       // ctypes drops the GIL: serialise
 
     BPE() {
         // GPT-2 bytes_to_unicode: printable Latin-1 bytes map to themselves, the rest to 256+n
@@ -308,9 +315,29 @@ struct BPE {
         return ids;
     }
 
+    int word_id(const std::string& w) {
+        uint32_t h = 2166136261u;  // FNV-1a
+        for (unsigned char c : w) h = (h ^ c) * 16777619u;
+        const int id = 256 + (int)(h % (uint32_t)(word_vocab - 257));
+        auto it = word_of.find(id);
+        if (it == word_of.end()) {
+            word_of.emplace(id, w);
+            return id;
+        }
+        return it->second == w ? id : -1;
+    }
+
     std::vector<int> encode(const std::string& text) {
+        std::lock_guard<std::mutex> g(mu);
         std::vector<int> ids;
         for (auto& w : pretokenize(text)) {
+            if (word_vocab > 257 && w.size() > 1) {
+                const int id = word_id(w);
+                if (id >= 0) {
+                    ids.push_back(id);
+                    continue;
+                }
+            }
             auto v = bpe_word(w);
             ids.insert(ids.end(), v.begin(), v.end());
         }
@@ -329,10 +356,18 @@ struct BPE {
         return s;
     }
 
-    std::string decode(const int* ids, int n) const {
+    std::string decode(const int* ids, int n) {
+        std::lock_guard<std::mutex> g(mu);
         std::string bytes;
         for (int k = 0; k < n; ++k) {
             int id = ids[k];
+            if (word_vocab) {
+                auto w = word_of.find(id);
+                if (w != word_of.end()) {
+                    bytes += w->second;
+                    continue;
+                }
+            }
             if (id >= 0 && id < (int)decoder.size() && !decoder[id].empty()) {
                 const std::string& t = decoder[id];
                 size_t i = 0;
@@ -521,6 +556,18 @@ void* dlms_bpe_create(const char* vocab_json, const char* merges_txt) {
 int dlms_bpe_is_synthetic(void* h) { return static_cast<BPE*>(h)->synthetic ? 1 : 0; }
 
 int dlms_bpe_vocab_size(void* h) { return static_cast<BPE*>(h)->vocab_size; }
+
+// synthetic vocabularies only: one hashed id per word, ids < vocab (the model's vocabulary;
+// id vocab-1 is left to <|endoftext|>).  Returns 0 on success.
+int dlms_bpe_set_synthetic_words(void* h, int vocab) {
+    BPE* b = static_cast<BPE*>(h);
+    if (!b->synthetic || vocab <= 512) return -1;
+    std::lock_guard<std::mutex> g(b->mu);
+    b->word_vocab = vocab;
+    b->vocab_size = vocab;
+    b->word_of.clear();
+    return 0;
+}
 
 // returns the number of ids (may exceed cap: call again with a larger buffer)
 int dlms_bpe_encode(void* h, const char* text, int len, int* out, int cap) {

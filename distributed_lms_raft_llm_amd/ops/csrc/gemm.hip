@@ -280,11 +280,12 @@ static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int
     return hipGetLastError();
 }
 
-// Tile selection, fit to the graph-replay sweep in profiles/r1_gemm_tile_sweep.jsonl (M = 256 and
-// 1024, GPT-2 shapes): a 2-deep LDS ring beats 3-4 deep at every shape (two workgroups per CU hide
-// the load latency better than one deeper ring), 64x64 wins wherever it yields < ~512
-// 128x128-tiles, and only grids with >= 512 128x128-tiles (LM head, prefill) amortise the bigger
-// tile's operand reuse.  The 8-wave variants never won and stay tuning-only.
+// Tile selection, fit to the COLD-weight graph-replay sweep (profiles/r1_gemm_tile_sweep_cold.jsonl:
+// weights rotated over >= 768 MB so they stream from HBM as in the 12-layer decode step; an
+// L2-hot sweep favours shallow rings and misled an earlier version).  Decode GEMMs below ~400
+// 64x64 workgroups are latency-bound on the K loop: keep 4-6 stages of LDS-DMA in flight; above
+// that, occupancy hides latency better than ring depth (2 stages, two workgroups per CU).  The LM
+// head (N = vocab) and prefill grids amortise 128x128 tiles.  8-wave variants stay tuning-only.
 static int g_force_tile = -1;  // tuning override (dlms_gemm_force_tile), -1 = heuristic
 
 template <int EPI>
@@ -325,9 +326,13 @@ static hipError_t launch_gemm_epi(const bf16_t* A, int lda, const bf16_t* W, int
         hipError_t e = launch_forced<EPI>(g_force_tile, A, lda, W, ldw, M, N, K, ep, stream, &done);
         if (done) return e;
     }
-    if (M <= 32) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    const long t128x128 = (long)((M + 127) / 128) * (N / 128) * split;
-    if (N % 128 == 0 && t128x128 >= 512) return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    const long t64 = (long)((M + 63) / 64) * (N / 64) * split;
+    const long t128 = (long)((M + 127) / 128) * (N / 128) * split;
+    if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
+        return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (M <= 64) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (t64 <= 400) return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     return launch_gemm_cfg<64, 64, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
 }
 

@@ -2,7 +2,9 @@
 
 ``GPT2BPE``      -- GPT-2 byte-level BPE (``tutoring_server.py:11,20,30``).  Pass the real
                     ``vocab.json``/``merges.txt`` to reproduce GPT-2 ids exactly; without them a
-                    synthetic byte-level vocabulary is used (no network for the real files).
+                    synthetic vocabulary is used (no network for the real files): byte tokens
+                    plus, by default, one hashed id per word, so a prompt's token count is close
+                    to real GPT-2's (the tutoring prompt template is ~25 tokens, not ~100 bytes).
 ``BertWordPiece``-- bert-base-uncased WordPiece (``lms_server.py:97-101``), ``vocab.txt`` or a
                     deterministic hashed synthetic vocabulary; ``[CLS] ... [SEP]``, truncation 512.
 """
@@ -17,7 +19,10 @@ EOS = "<|endoftext|>"
 
 
 class GPT2BPE:
-    def __init__(self, vocab_json: str | None = None, merges_txt: str | None = None, eos_token_id: int = 50256):
+    def __init__(self, vocab_json: str | None = None, merges_txt: str | None = None, eos_token_id: int = 50256,
+                 synthetic_words: bool = True, vocab_size: int | None = None):
+        """``vocab_size``: the model's vocabulary (synthetic word ids stay below it); default
+        ``eos_token_id + 1`` (GPT-2's EOS is its last id)."""
         vocab_json = vocab_json or os.environ.get("DLMS_GPT2_VOCAB")
         merges_txt = merges_txt or os.environ.get("DLMS_GPT2_MERGES")
         L = native.lib()
@@ -27,6 +32,9 @@ class GPT2BPE:
             raise ValueError(f"could not load BPE vocabulary {vocab_json!r} / {merges_txt!r}")
         self.synthetic = bool(L.dlms_bpe_is_synthetic(self._h))
         self.eos_token_id = eos_token_id
+        self.synthetic_words = False
+        if self.synthetic and synthetic_words and (vocab_size or eos_token_id + 1) > 512:
+            self.synthetic_words = L.dlms_bpe_set_synthetic_words(self._h, vocab_size or eos_token_id + 1) == 0
 
     def encode(self, text: str) -> list[int]:
         L = native.lib()

@@ -24,16 +24,17 @@ TILES = {-1: "auto", 0: "32x64s6", 1: "64x64s4", 2: "128x64s3", 3: "128x128s3", 
 
 
 def graph_time(fn, inner=20, reps=15):
+    """``fn(i)`` is launch i of the captured sequence (lets cold-weight runs rotate buffers)."""
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        for _ in range(3):
-            fn()
+        for i in range(3):
+            fn(i)
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        for _ in range(inner):
-            fn()
+        for i in range(inner):
+            fn(i)
     g.replay()
     torch.cuda.synchronize()
     ts = []
@@ -54,7 +55,12 @@ def main():
     ap.add_argument("--batches", default="64,256,512")
     ap.add_argument("--tiles", default="-1,1,2,3,4,5,7")
     ap.add_argument("--T", type=int, default=150)
+    ap.add_argument("--cold-mb", type=int, default=768,
+                    help="rotate GEMM weights over >= this many MB per graph so they stream from HBM like "
+                         "the 12-layer decode step (0: one L2/MALL-hot weight)")
+    ap.add_argument("--ops", default="qkv,oproj,fc,proj,lmhead,attn,add_ln")
     args = ap.parse_args()
+    ops_on = set(args.ops.split(","))
     L = ops.lib()
     dev = "cuda"
     d = args.d
@@ -70,42 +76,51 @@ def main():
     for M in [int(x) for x in args.batches.split(",")]:
         a = torch.randn(M, d, device=dev).to(torch.bfloat16)
         a4 = torch.randn(M, 4 * d, device=dev).to(torch.bfloat16)
+
+        def weights(N, K):
+            n = 1 if not args.cold_mb else max(1, min(640, -(-args.cold_mb * 2**20 // (N * K * 2))))
+            base = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            return [base] + [base.clone() for _ in range(n - 1)]
+
         shapes = {
-            "qkv": (a, torch.randn(3 * d, d, device=dev).to(torch.bfloat16) * 0.02),
-            "oproj": (a, torch.randn(d, d, device=dev).to(torch.bfloat16) * 0.02),
-            "fc": (a, torch.randn(4 * d, d, device=dev).to(torch.bfloat16) * 0.02),
-            "proj": (a4, torch.randn(d, 4 * d, device=dev).to(torch.bfloat16) * 0.02),
-            "lmhead": (a, torch.randn(V, d, device=dev).to(torch.bfloat16) * 0.02),
+            "qkv": (a, (3 * d, d)), "oproj": (a, (d, d)), "fc": (a, (4 * d, d)), "proj": (a4, (d, 4 * d)),
+            "lmhead": (a, (V, d)),
         }
         parts = torch.empty(8, M, d, device=dev)
         keys = torch.zeros(M, V // 64, dtype=torch.int64, device=dev)
         seen = torch.zeros(M, V // 32, dtype=torch.int32, device=dev)
         out_bf = torch.empty(M, V, dtype=torch.bfloat16, device=dev)
-        for name, (x, w) in shapes.items():
-            N, K = w.shape
+        for name, (x, (N, K)) in shapes.items():
+            if name not in ops_on:
+                continue
+            ws = weights(N, K)
+            nw = len(ws)
+            inner = max(20, nw)
             variants = []
             if name in ("oproj", "proj"):
                 for s in (1, 2, 4, 8):
                     if (K // 64) % s == 0:
-                        variants.append((f"split{s}", lambda x=x, w=w, s=s: ops.gemm(x, w, ops.EPI_PARTIAL, out=parts,
-                                                                                   split_k=s)))
+                        variants.append((f"split{s}", lambda i, x=x, s=s: ops.gemm(x, ws[i % nw], ops.EPI_PARTIAL,
+                                                                                   out=parts, split_k=s)))
             elif name == "lmhead":
-                variants.append(("argmax", lambda x=x, w=w: ops.gemm(x, w, ops.EPI_ARGMAX, argmax_out=keys, seen=seen,
-                                                                     vocab=50257, penalty=1.2)))
-                variants.append(("bf16out", lambda x=x, w=w, N=N: ops.gemm(x, w, ops.EPI_BF16, out=out_bf[:, :N])))
+                variants.append(("argmax", lambda i, x=x: ops.gemm(x, ws[i % nw], ops.EPI_ARGMAX, argmax_out=keys,
+                                                                   seen=seen, vocab=50257, penalty=1.2)))
             else:
-                variants.append(("bf16", lambda x=x, w=w, N=N: ops.gemm(x, w, ops.EPI_BF16, out=out_bf[:, :N])))
+                variants.append(("bf16", lambda i, x=x, N=N: ops.gemm(x, ws[i % nw], ops.EPI_BF16, out=out_bf[:, :N])))
             for vname, fn in variants:
                 for t in tiles:
                     L.dlms_gemm_force_tile(t)
                     try:
-                        med, mn = graph_time(fn)
+                        med, mn = graph_time(fn, inner=inner)
                     finally:
                         L.dlms_gemm_force_tile(-1)
                     flops = 2 * M * N * K
                     byts = (M * K + N * K) * 2
                     rec(M=M, op=name, variant=vname, tile=TILES[t], us=round(med, 2), us_min=round(mn, 2),
-                        tflops=round(flops / med / 1e6, 1), GBps=round(byts / med / 1e3, 1))
+                        tflops=round(flops / med / 1e6, 1), GBps=round(byts / med / 1e3, 1), weight_copies=nw)
+            del ws
+        if "attn" not in ops_on and "add_ln" not in ops_on:
+            continue
         kc = torch.randn(M, H, args.T, 64, device=dev).to(torch.bfloat16)
         vc = torch.randn(M, H, args.T, 64, device=dev).to(torch.bfloat16)
         q = torch.randn(M, d, device=dev).to(torch.bfloat16)
@@ -114,7 +129,9 @@ def main():
         for Lk in (32, 90, args.T):
             kvl = torch.full((M,), Lk, dtype=torch.int32, device=dev)
             for impl in ("wave", "lds"):
-                med, mn = graph_time(lambda impl=impl: ops.row_attention(q, kc, vc, slot, kvl, out=o, impl=impl))
+                if "attn" not in ops_on:
+                    break
+                med, mn = graph_time(lambda i, impl=impl: ops.row_attention(q, kc, vc, slot, kvl, out=o, impl=impl))
                 byts = M * H * Lk * 64 * 2 * 2
                 rec(M=M, op="attn", variant=f"{impl}_T{Lk}", us=round(med, 2), us_min=round(mn, 2),
                     GBps=round(byts / med / 1e3, 1))
@@ -123,7 +140,9 @@ def main():
         b = torch.zeros(d, device=dev)
         h = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
         for s in (0, 4, 8):
-            med, mn = graph_time(lambda s=s: ops.add_layernorm(x, g, b, 1e-5, parts=parts if s else None, nsplit=s,
+            if "add_ln" not in ops_on:
+                break
+            med, mn = graph_time(lambda i, s=s: ops.add_layernorm(x, g, b, 1e-5, parts=parts if s else None, nsplit=s,
                                                                bias=b, out_bf16=h))
             rec(M=M, op="add_ln", variant=f"split{s}", us=round(med, 2), us_min=round(mn, 2))
     print("SUMMARY " + json.dumps(res))

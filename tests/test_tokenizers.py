@@ -48,7 +48,7 @@ def test_bpe_matches_hf_on_same_files(bpe_files):
 
 
 def test_bpe_synthetic_roundtrip_and_prompt_template():
-    t = GPT2BPE()
+    t = GPT2BPE(synthetic_words=False)
     assert t.synthetic
     prompt = "You are an intelligent assistant. Answer the following question in detail:\nQuestion: hi\nAnswer:"
     ids = t.encode(prompt)
@@ -60,6 +60,20 @@ def test_bpe_synthetic_roundtrip_and_prompt_template():
     assert t.encode("a<|endoftext|>b") == t.encode("a") + [50256] + t.encode("b")
     txt = t.decode([300, 4000, 50000])
     assert txt and txt.isprintable()
+
+
+def test_bpe_synthetic_word_mode_lengths_and_roundtrip():
+    t = GPT2BPE()
+    assert t.synthetic and t.synthetic_words
+    prompt = "You are an intelligent assistant. Answer the following question in detail:\nQuestion: hi\nAnswer:"
+    ids = t.encode(prompt)
+    assert 15 <= len(ids) <= 30  # real GPT-2 BPE: 23 tokens; byte level would be 93
+    assert all(0 <= i < 50256 for i in ids)
+    assert t.decode(ids) == prompt and t.encode(prompt) == ids
+    # a small model vocabulary bounds the ids (gpt2-tiny: 1000 ids, EOS 999)
+    tiny = GPT2BPE(eos_token_id=999)
+    tids = tiny.encode(prompt + " and some more words to collide")
+    assert max(tids) < 999 and tiny.decode(tids) == prompt + " and some more words to collide"
 
 
 @pytest.fixture(scope="module")
