@@ -128,49 +128,73 @@ extern "C" hipError_t dlms_layernorm_gather(const float* x, int ldx, const int* 
 //     out = bf16(LN(v) * gamma + beta)               (skipped when out == nullptr)
 // This consumes the split-K partial slabs of the previous projection GEMM (EPI_PARTIAL) or, under
 // tensor parallelism, the all-reduced partial, so no GEMM epilogue ever read-modify-writes x.
-template <int NSPLIT>
-__global__ __launch_bounds__(64) void add_layernorm_kernel(float* x, int ldx, const float* __restrict__ parts,
-                                                           int ldp, long long split_stride,
-                                                           const float* __restrict__ bias,
+template <int NSPLIT, int NV4>
+__global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x, int ldx,
+                                                           const float* __restrict__ parts, int ldp,
+                                                           long long split_stride, const float* __restrict__ bias,
                                                            const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, bf16_t* out, int ldb,
-                                                           int M, int D, float eps, int store_normed) {
+                                                           const float* __restrict__ beta, bf16_t* __restrict__ out,
+                                                           int ldb, int M, int D, float eps, int store_normed) {
     const int lane = threadIdx.x;
     const int row = blockIdx.x;
     if (row >= M) return;
     const int nv = D >> 2;
     float4* xr = reinterpret_cast<float4*>(x + (size_t)row * ldx);
     const bool update = (NSPLIT > 0 || bias != nullptr) && !store_normed;
-    float4 v[LN_MAX_V4];
+    // Branch-free and load-first: NV4 (= ceil(D / 256)) float4 per lane at compile time, column
+    // index clamped (the tail's duplicate loads are masked afterwards), and every load of the row
+    // -- residual, bias, all split-K partials -- issued before any use or store.  A data-dependent
+    // `if (c < nv)` around each load made the compiler wait on each one in turn (NSPLIT x NV4
+    // serialised memory latencies, ~7 us for d=768 at 8 splits).
+    int cidx[NV4];
+    bool valid[NV4];
+#pragma unroll
+    for (int i = 0; i < NV4; ++i) {
+        const int c = lane + i * 64;
+        valid[i] = c < nv;
+        cidx[i] = valid[i] ? c : nv - 1;
+    }
+    float4 v[NV4];
+#pragma unroll
+    for (int i = 0; i < NV4; ++i) v[i] = xr[cidx[i]];
+    float4 pv[NSPLIT > 0 ? NSPLIT : 1][NV4];
+#pragma unroll
+    for (int k = 0; k < NSPLIT; ++k) {
+        const float4* pk = reinterpret_cast<const float4*>(parts + (size_t)k * split_stride + (size_t)row * ldp);
+#pragma unroll
+        for (int i = 0; i < NV4; ++i) pv[k][i] = pk[cidx[i]];
+    }
+    if (bias) {
+#pragma unroll
+        for (int i = 0; i < NV4; ++i) {
+            const float4 b = reinterpret_cast<const float4*>(bias)[cidx[i]];
+            v[i].x += b.x; v[i].y += b.y; v[i].z += b.z; v[i].w += b.w;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NSPLIT; ++k) {
+#pragma unroll
+        for (int i = 0; i < NV4; ++i) {
+            v[i].x += pv[k][i].x; v[i].y += pv[k][i].y; v[i].z += pv[k][i].z; v[i].w += pv[k][i].w;
+        }
+    }
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAX_V4; ++i) {
-        const int c = lane + i * 64;
-        if (c < nv) {
-            float4 a = xr[c];
-            if (bias) {
-                const float4 b = reinterpret_cast<const float4*>(bias)[c];
-                a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-            }
-#pragma unroll
-            for (int k = 0; k < NSPLIT; ++k) {
-                const float4 p = reinterpret_cast<const float4*>(parts + (size_t)k * split_stride + (size_t)row * ldp)[c];
-                a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
-            }
-            if (update) xr[c] = a;
-            v[i] = a;
-        } else {
-            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+    for (int i = 0; i < NV4; ++i) {
+        if (!valid[i]) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    if (update) {
+#pragma unroll
+        for (int i = 0; i < NV4; ++i)
+            if (valid[i]) xr[cidx[i]] = v[i];
     }
     if (out == nullptr && !store_normed) return;
     const float mean = wave_sum(s) / (float)D;
     float ss = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAX_V4; ++i) {
-        const int c = lane + i * 64;
-        if (c < nv) {
+    for (int i = 0; i < NV4; ++i) {
+        if (valid[i]) {
             const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
             ss += (a * a + b * b) + (cc * cc + d * d);
         }
@@ -179,21 +203,35 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* x, int ldx, co
     const float4* g4 = reinterpret_cast<const float4*>(gamma);
     const float4* b4 = reinterpret_cast<const float4*>(beta);
 #pragma unroll
-    for (int i = 0; i < LN_MAX_V4; ++i) {
-        const int c = lane + i * 64;
-        if (c < nv) {
-            const float4 g = g4[c], b = b4[c];
-            uint2 p;
-            p.x = pack_bf16x2((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y);
-            p.y = pack_bf16x2((v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
-            if (out) reinterpret_cast<uint2*>(out + (size_t)row * ldb)[c] = p;
-            if (store_normed) {  // post-LN residual stream (BERT): x <- LN(x + ...)
-                const float4 y = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
-                                             (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
-                xr[c] = y;
+    for (int i = 0; i < NV4; ++i) {
+        const float4 g = g4[cidx[i]], b = b4[cidx[i]];
+        if (valid[i]) {
+            const float4 y = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
+                                         (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+            if (out) {
+                uint2 p;
+                p.x = pack_bf16x2(y.x, y.y);
+                p.y = pack_bf16x2(y.z, y.w);
+                reinterpret_cast<uint2*>(out + (size_t)row * ldb)[cidx[i]] = p;
             }
+            if (store_normed) xr[cidx[i]] = y;  // post-LN residual stream (BERT): x <- LN(x + ...)
         }
     }
+}
+
+template <int NSPLIT>
+static void launch_add_ln(int nv4, dim3 grid, hipStream_t stream, float* x, int ldx, const float* parts, int ldp,
+                          long long split_stride, const float* bias, const float* gamma, const float* beta,
+                          bf16_t* o, int ldb, int M, int D, float eps, int store_normed) {
+#define ADD_LN_V(V)                                                                                            \
+    case V:                                                                                                    \
+        hipLaunchKernelGGL((add_layernorm_kernel<NSPLIT, V>), grid, dim3(64), 0, stream, x, ldx, parts, ldp,    \
+                           split_stride, bias, gamma, beta, o, ldb, M, D, eps, store_normed);                  \
+        break;
+    switch (nv4) {
+        ADD_LN_V(1) ADD_LN_V(2) ADD_LN_V(3) ADD_LN_V(4) ADD_LN_V(5) ADD_LN_V(6) ADD_LN_V(7) ADD_LN_V(8)
+    }
+#undef ADD_LN_V
 }
 
 extern "C" hipError_t dlms_add_layernorm(float* x, int ldx, const float* parts, int ldp, long long split_stride,
@@ -202,10 +240,11 @@ extern "C" hipError_t dlms_add_layernorm(float* x, int ldx, const float* parts, 
                                          hipStream_t stream) {
     if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0 || nsplit < 0 || nsplit > 8) return hipErrorInvalidValue;
     bf16_t* o = reinterpret_cast<bf16_t*>(out_bf16);
+    const int nv4 = (D / 4 + 63) / 64;
 #define ADD_LN_CASE(NS)                                                                                       \
     case NS:                                                                                                  \
-        hipLaunchKernelGGL(add_layernorm_kernel<NS>, dim3(M), dim3(64), 0, stream, x, ldx, parts, ldp, split_stride, \
-                           bias, gamma, beta, o, ldb, M, D, eps, store_normed);                                             \
+        launch_add_ln<NS>(nv4, dim3(M), stream, x, ldx, parts, ldp, split_stride, bias, gamma, beta, o, ldb, M, D, \
+                          eps, store_normed);                                                                 \
         break;
     switch (nsplit) {
         ADD_LN_CASE(0) ADD_LN_CASE(1) ADD_LN_CASE(2) ADD_LN_CASE(3) ADD_LN_CASE(4) ADD_LN_CASE(5) ADD_LN_CASE(6)
