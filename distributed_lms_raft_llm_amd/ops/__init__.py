@@ -64,6 +64,9 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB_PATH
 
 
+FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), not the MI300 fnuz variant
+
+
 class GemmEpi(ctypes.Structure):
     _fields_ = [
         ("bias", ctypes.c_void_p), ("out", ctypes.c_void_p), ("ldo", ctypes.c_int),
@@ -76,6 +79,7 @@ class GemmEpi(ctypes.Structure):
         ("seen_words", ctypes.c_int), ("vocab", ctypes.c_int), ("col_offset", ctypes.c_int),
         ("penalty", ctypes.c_float),
         ("split_k", ctypes.c_int), ("split_stride", ctypes.c_longlong),
+        ("a_scale", ctypes.c_void_p), ("w_scale", ctypes.c_void_p),
     ]
 
 
@@ -83,9 +87,11 @@ def _bind(L):
     P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     sig = {
         "dlms_gemm": [I, P, I, P, I, I, I, I, ctypes.POINTER(GemmEpi), P],
+        "dlms_gemm_fp8": [I, P, I, P, I, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_layernorm": [P, I, P, P, P, I, P, I, I, I, F, P],
         "dlms_layernorm_gather": [P, I, P, P, P, P, I, I, I, F, P],
-        "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, I, I, F, I, P],
+        "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, P, I, P, I, I, F, I, P],
+        "dlms_quantize_rows_fp8": [P, I, P, I, P, I, I, P],
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
@@ -161,15 +167,25 @@ def _req(t: torch.Tensor, dtype, name: str, dim: int | None = None):
 def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, out=None, resid=None,
          q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
          argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0,
-         split_k: int = 1):
-    """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0)."""
-    _req(a, torch.bfloat16, "a", 2)
-    _req(w, torch.bfloat16, "w", 2)
+         split_k: int = 1, a_scale=None, w_scale=None):
+    """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0).
+    fp8 (W8A8): a and w ``torch.float8_e4m3fn`` with f32 ``a_scale`` [M] and ``w_scale`` [N]
+    (C = diag(a_scale) (a @ w.T) diag(w_scale)); K % 128 == 0."""
+    fp8 = a.dtype == FP8
+    _req(a, FP8 if fp8 else torch.bfloat16, "a", 2)
+    _req(w, FP8 if fp8 else torch.bfloat16, "w", 2)
     M, K = a.shape
     N, K2 = w.shape
-    if K != K2 or K % 64 or N % 64:
-        raise ValueError(f"gemm shapes a{tuple(a.shape)} w{tuple(w.shape)}: need matching K%64==0, N%64==0")
+    if K != K2 or K % (128 if fp8 else 64) or N % 64:
+        raise ValueError(f"gemm shapes a{tuple(a.shape)} w{tuple(w.shape)}: need matching K%64==0 (fp8: 128), "
+                         f"N%64==0")
     ep = GemmEpi()
+    if fp8:
+        _req(a_scale, torch.float32, "a_scale", 1)
+        _req(w_scale, torch.float32, "w_scale", 1)
+        if a_scale.numel() < M or w_scale.numel() < N:
+            raise ValueError("fp8 scales too short")
+        ep.a_scale, ep.w_scale = a_scale.data_ptr(), w_scale.data_ptr()
     if bias is not None:
         _req(bias, torch.float32, "bias", 1)
         if bias.numel() < N:
@@ -208,7 +224,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         ep.n_heads, ep.t_max, ep.d_local = k_cache.shape[1], k_cache.shape[2], d_local
         out = q_out
     elif epi == EPI_PARTIAL:
-        if split_k < 1 or K % (64 * split_k):
+        if split_k < 1 or K % ((128 if fp8 else 64) * split_k):
             raise ValueError(f"split_k={split_k} must divide K/64 (K={K})")
         if out is None:
             out = torch.empty(split_k, M, N, dtype=torch.float32, device=a.device)
@@ -229,10 +245,40 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         out = argmax_out
     else:
         raise ValueError(f"unknown epilogue {epi}")
-    _check(lib().dlms_gemm(epi, _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, ctypes.byref(ep), _stream()),
-           "dlms_gemm")
+    if fp8:
+        if epi in (EPI_GELU_ERF, EPI_F32):
+            raise ValueError("fp8 GEMM: epilogue not instantiated")
+        _check(lib().dlms_gemm_fp8(epi, _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, ctypes.byref(ep),
+                                   _stream()), "dlms_gemm_fp8")
+    else:
+        _check(lib().dlms_gemm(epi, _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, ctypes.byref(ep), _stream()),
+               "dlms_gemm")
     return out
 
+
+def quantize_fp8_rows(a: torch.Tensor, out=None, scale=None):
+    """bf16 [M, D] -> (e4m3 [M, D], f32 row scales [M]) with scale = absmax / 448 (HIP kernel)."""
+    _req(a, torch.bfloat16, "a", 2)
+    M, D = a.shape
+    if D % 4:
+        raise ValueError("quantize_fp8_rows: D % 4")
+    out = torch.empty(M, D, dtype=FP8, device=a.device) if out is None else out
+    scale = torch.empty(M, dtype=torch.float32, device=a.device) if scale is None else scale
+    _req(out, FP8, "out", 2)
+    _req(scale, torch.float32, "scale", 1)
+    if out.shape[0] < M or out.shape[1] < D or scale.numel() < M or out.stride(0) % 4:
+        raise ValueError("quantize_fp8_rows: outputs too small / misaligned")
+    _check(lib().dlms_quantize_rows_fp8(_p(a), a.stride(0), _p(out), out.stride(0), _p(scale), M, D, _stream()),
+           "dlms_quantize_rows_fp8")
+    return out, scale
+
+
+def quantize_fp8_weight(w: torch.Tensor):
+    """Host/torch-side weight quantisation: per-output-channel (row) scale = absmax / 448."""
+    wf = w.float()
+    scale = (wf.abs().amax(dim=1).clamp_min(1e-20) / 448.0)
+    q = (wf / scale[:, None]).clamp(-448.0, 448.0).to(FP8)
+    return q.contiguous(), scale.contiguous()
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, *, out_bf16=None,
               out_f32=None, want_bf16: bool = True):
@@ -261,9 +307,11 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
 
 def add_layernorm(x: torch.Tensor, gamma, beta, eps: float, *, parts: torch.Tensor | None = None, nsplit: int = 0,
                   bias: torch.Tensor | None = None, out_bf16: torch.Tensor | None = None, want_out: bool = True,
-                  store_normed: bool = False):
+                  store_normed: bool = False, out_fp8: torch.Tensor | None = None,
+                  out_fp8_scale: torch.Tensor | None = None):
     """v = x + bias + sum(parts[:nsplit]); x <- v (or LN(v) when ``store_normed``: post-LN models);
-    out = bf16(LN(v)).  parts: f32 [S, >=M, >=D]."""
+    out = bf16(LN(v)); optionally also the row-scaled e4m3 copy (``out_fp8`` + ``out_fp8_scale``)
+    that feeds an fp8 GEMM.  parts: f32 [S, >=M, >=D]."""
     _req(x, torch.float32, "x", 2)
     M, D = x.shape
     if D % 4 or D > 2048 or gamma.numel() != D or beta.numel() != D:
@@ -284,10 +332,17 @@ def add_layernorm(x: torch.Tensor, gamma, beta, eps: float, *, parts: torch.Tens
         _req(out_bf16, torch.bfloat16, "out_bf16", 2)
         if out_bf16.shape[0] < M or out_bf16.shape[1] < D:
             raise ValueError("add_layernorm: out too small")
+    ld8 = 0
+    if out_fp8 is not None:
+        _req(out_fp8, FP8, "out_fp8", 2)
+        _req(out_fp8_scale, torch.float32, "out_fp8_scale", 1)
+        if out_fp8.shape[0] < M or out_fp8.shape[1] < D or out_fp8_scale.numel() < M or out_fp8.stride(0) % 4:
+            raise ValueError("add_layernorm: fp8 outputs too small / misaligned")
+        ld8 = out_fp8.stride(0)
     _check(lib().dlms_add_layernorm(_p(x), x.stride(0), _p(parts) if nsplit else None, ldp, sstride, nsplit,
                                     _p(bias), _p(gamma), _p(beta), _p(out_bf16),
-                                    out_bf16.stride(0) if out_bf16 is not None else 0, M, D, float(eps),
-                                    int(store_normed), _stream()),
+                                    out_bf16.stride(0) if out_bf16 is not None else 0, _p(out_fp8), ld8,
+                                    _p(out_fp8_scale), M, D, float(eps), int(store_normed), _stream()),
            "dlms_add_layernorm")
     return out_bf16
 

@@ -128,4 +128,7 @@ struct GemmEpi {
     // at out + s * split_stride (elements).  Summed later by the fused add+LayerNorm kernel.
     int split_k;
     long long split_stride;
+    // fp8 inputs (dlms_gemm_fp8): per-row activation and per-output-channel weight scales
+    const float* a_scale;
+    const float* w_scale;
 };

@@ -16,6 +16,10 @@
 //                                                                in-place when out == resid
 //   EPI_QKV         q -> q_out, k/v scattered into the KV cache at (slot,pos) of each row (K3+K4)
 //   EPI_ARGMAX      repetition-penalised logits -> per-row packed (value,index) atomicMax (K10-K12)
+//   (IN = IN_FP8: A and W are OCP e4m3 with per-row / per-output-channel fp32 scales; the same
+//   128-B LDS rows then hold 128 k-elements, each 16-B fragment feeds two
+//   v_mfma_f32_16x16x32_fp8_fp8, and acc is rescaled by a_scale[row] * w_scale[col] before the
+//   epilogue.  W8A8 halves the weight bytes the latency-bound decode GEMMs stream.)
 //   EPI_PARTIAL     split-K: slice s stores its raw fp32 partial tile; the following fused
 //                   residual-add + LayerNorm kernel sums the slices in a fixed order (deterministic,
 //                   no atomics) -- the decode projections with N = d are split 2-4 ways so the
@@ -26,7 +30,8 @@ enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV =
 
 // struct GemmEpi lives in common.h (shared with the ABI probe in api.hip)
 
-#define GEMM_BK 64
+#define GEMM_BK 64  // k-elements per ring step for bf16 (128 for fp8: the row is 128 B either way)
+enum { IN_BF16 = 0, IN_FP8 = 1 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glob_void_t;
@@ -45,10 +50,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Synchronisation: counted `s_waitcnt vmcnt` + raw s_barrier (a __syncthreads() would drain the
 // in-flight DMA every step); out-of-range A rows read a clamped valid row (their results are never
 // stored), so the DMA never needs predication.
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __restrict__ A, int lda,
-                                                      const bf16_t* __restrict__ W, int ldw, int M, int N,
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __restrict__ A, int lda,
+                                                      const void* __restrict__ W, int ldw, int M, int N,
                                                       int K, GemmEpi ep) {
+    constexpr int EB = IN == IN_FP8 ? 1 : 2;    // bytes per element
+    constexpr int BKE = GEMM_BK * 2 / EB;       // k-elements per ring step
     constexpr int NW = WM * WN;  // waves per workgroup (4 or 8)
     constexpr int NT = 64 * NW;
     static_assert(NW == 4 || NW == 8, "4 or 8 waves per workgroup");
@@ -86,8 +93,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __r
     const int k_len = K / nsplit;
     const int k_base = split * k_len;
 
-    // per-lane DMA sources (fixed for the K loop)
-    const bf16_t* src[PPW];
+    // per-lane DMA sources (fixed for the K loop; byte addresses)
+    const char* src[PPW];
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
         const int piece = wave + NW * i;
@@ -95,17 +102,17 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __r
         const int lchunk = (lane & 7) ^ (lane >> 3);
         if (row < BM) {
             const int gm = m0 + row < M ? m0 + row : M - 1;
-            src[i] = A + (size_t)gm * lda + k_base + lchunk * 8;
+            src[i] = reinterpret_cast<const char*>(A) + ((size_t)gm * lda + k_base) * EB + lchunk * 16;
         } else {
-            src[i] = W + (size_t)(n0 + row - BM) * ldw + k_base + lchunk * 8;
+            src[i] = reinterpret_cast<const char*>(W) + ((size_t)(n0 + row - BM) * ldw + k_base) * EB + lchunk * 16;
         }
     }
     auto issue = [&](int stage, int k0) {
         char* dst = smem + stage * STAGE_BYTES;
 #pragma unroll
         for (int i = 0; i < PPW; ++i)
-            __builtin_amdgcn_global_load_lds((glob_void_t*)(src[i] + k0), (lds_void_t*)(dst + (wave + NW * i) * 1024),
-                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((glob_void_t*)(src[i] + (size_t)k0 * EB),
+                                             (lds_void_t*)(dst + (wave + NW * i) * 1024), 16, 0, 0);
     };
 
     f32x4_t acc[TM][TN];
@@ -114,12 +121,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __r
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-    const int nk = k_len / GEMM_BK;
+    const int nk = k_len / BKE;
     // prologue: up to STAGES-1 steps in flight; no step is ever loaded twice (short split-K slices
     // would otherwise multiply their traffic)
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) issue(s, s * GEMM_BK);
+        if (s < nk) issue(s, s * BKE);
 
     const int frow = lane & 15;
     const int fk = lane >> 4;
@@ -136,28 +143,70 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __r
         asm volatile("" ::: "memory");
         {
             const int kn = kt + STAGES - 1;
-            if (kn < nk) issue(kn % STAGES, kn * GEMM_BK);
+            if (kn < nk) issue(kn % STAGES, kn * BKE);
         }
         const char* as = smem + (kt % STAGES) * STAGE_BYTES + (wm * WTM) * ROWB;
         const char* ws = smem + (kt % STAGES) * STAGE_BYTES + A_BYTES + (wn * WTN) * ROWB;
 #pragma unroll
-        for (int ks = 0; ks < GEMM_BK / 32; ++ks) {
+        for (int ks = 0; ks < 2; ++ks) {
             const int coff = (((ks * 4 + fk) ^ fsw) << 4);
-            bf16x8_t af[TM], bfr[TN];
+            if constexpr (IN == IN_FP8) {
+                // a 16-B chunk = 16 k-elements: bytes 0-7 feed one fp8 MFMA, bytes 8-15 the next.
+                // A and W use the same k permutation, so the dot products are unchanged.
+                long af[TM][2], bfr[TN][2];
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-                af[i] = *reinterpret_cast<const bf16x8_t*>(as + (i * 16 + frow) * ROWB + coff);
+                for (int i = 0; i < TM; ++i) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(as + (i * 16 + frow) * ROWB + coff);
+                    af[i][0] = (long)(((unsigned long long)v.y << 32) | v.x);
+                    af[i][1] = (long)(((unsigned long long)v.w << 32) | v.z);
+                }
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                bfr[j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frow) * ROWB + coff);
+                for (int j = 0; j < TN; ++j) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ws + (j * 16 + frow) * ROWB + coff);
+                    bfr[j][0] = (long)(((unsigned long long)v.y << 32) | v.x);
+                    bfr[j][1] = (long)(((unsigned long long)v.w << 32) | v.z);
+                }
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af[i][h], bfr[j][h], acc[i][j],
+                                                                                   0, 0, 0);
+            } else {
+                bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8_t*>(as + (i * 16 + frow) * ROWB + coff);
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    bfr[j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frow) * ROWB + coff);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
         }
     }
     wait_vmcnt<0>();  // drain the tail DMA before the workgroup may exit / LDS be reused
+
+    if constexpr (IN == IN_FP8) {  // dequantise: per-row activation scale x per-channel weight scale
+        const int rb = m0 + wm * WTM + (lane >> 4) * 4;
+        const int cb = n0 + wn * WTN + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const float wsc = ep.w_scale[cb + j * 16];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = rb + i * 16 + r;
+                    acc[i][j][r] *= ep.a_scale[row < M ? row : M - 1] * wsc;
+                }
+            }
+    }
 
     // ---------------- epilogue ----------------
     // accumulator element r of tile (i,j): row = (lane>>4)*4 + r, col = lane & 15
@@ -262,19 +311,19 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const bf16_t* __r
     }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
-static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN>
+static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
     const int tiles = ((M + BM - 1) / BM) * (N / BN) * (EPI == EPI_PARTIAL ? ep.split_k : 1);
-    const size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * sizeof(bf16_t);
+    const size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI>), dim3(tiles), dim3(64 * WM * WN), lds, stream, A,
+    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN>), dim3(tiles), dim3(64 * WM * WN), lds, stream, A,
                        lda, W,
                        ldw, M, N, K, ep);
     return hipGetLastError();
@@ -288,52 +337,52 @@ static hipError_t launch_gemm_cfg(const bf16_t* A, int lda, const bf16_t* W, int
 // head (N = vocab) and prefill grids amortise 128x128 tiles.  8-wave variants stay tuning-only.
 static int g_force_tile = -1;  // tuning override (dlms_gemm_force_tile), -1 = heuristic
 
-template <int EPI>
-static hipError_t launch_forced(int id, const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
+template <int EPI, int IN>
+static hipError_t launch_forced(int id, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                 const GemmEpi& ep, hipStream_t stream, bool* done) {
     *done = true;
     switch (id) {
-        case 0: return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-        case 1: return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-        case 2: return launch_gemm_cfg<128, 64, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-        case 4: return launch_gemm_cfg<64, 64, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-        case 7: return launch_gemm_cfg<64, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 0: return launch_gemm_cfg<32, 64, 2, 2, 6, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 1: return launch_gemm_cfg<64, 64, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 2: return launch_gemm_cfg<128, 64, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 4: return launch_gemm_cfg<64, 64, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+        case 7: return launch_gemm_cfg<64, 64, 2, 2, 6, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
         default: break;
     }
     if (N % 128 == 0) {
         switch (id) {
-            case 3: return launch_gemm_cfg<128, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-            case 5: return launch_gemm_cfg<64, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-            case 6: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 3: return launch_gemm_cfg<128, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 5: return launch_gemm_cfg<64, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 6: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             // 8-wave workgroups: two waves per SIMD, one's LDS reads under the other's MFMAs
-            case 8: return launch_gemm_cfg<256, 128, 4, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-            case 10: return launch_gemm_cfg<128, 128, 4, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-            case 11: return launch_gemm_cfg<128, 128, 2, 4, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 8: return launch_gemm_cfg<256, 128, 4, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 10: return launch_gemm_cfg<128, 128, 4, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 11: return launch_gemm_cfg<128, 128, 2, 4, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             default: break;
         }
     }
-    if (N % 256 == 0 && id == 9) return launch_gemm_cfg<128, 256, 2, 4, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (N % 256 == 0 && id == 9) return launch_gemm_cfg<128, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     *done = false;
     return hipSuccess;
 }
 
-template <int EPI>
-static hipError_t launch_gemm_epi(const bf16_t* A, int lda, const bf16_t* W, int ldw, int M, int N, int K,
+template <int EPI, int IN>
+static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
     const int split = EPI == EPI_PARTIAL ? ep.split_k : 1;
     if (g_force_tile >= 0) {
         bool done = false;
-        hipError_t e = launch_forced<EPI>(g_force_tile, A, lda, W, ldw, M, N, K, ep, stream, &done);
+        hipError_t e = launch_forced<EPI, IN>(g_force_tile, A, lda, W, ldw, M, N, K, ep, stream, &done);
         if (done) return e;
     }
     const long t64 = (long)((M + 63) / 64) * (N / 64) * split;
     const long t128 = (long)((M + 127) / 128) * (N / 128) * split;
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
-        return launch_gemm_cfg<128, 128, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    if (M <= 64) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    if (t64 <= 400) return launch_gemm_cfg<64, 64, 2, 2, 4, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    return launch_gemm_cfg<64, 64, 2, 2, 2, EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+        return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (M <= 64) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (t64 <= 400) return launch_gemm_cfg<64, 64, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    return launch_gemm_cfg<64, 64, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
 }
 
 extern "C" void dlms_gemm_force_tile(int id) { g_force_tile = id; }
@@ -342,16 +391,31 @@ extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, 
                                 const GemmEpi* ep, hipStream_t stream) {
     if (K % GEMM_BK != 0 || N % 64 != 0 || M <= 0) return hipErrorInvalidValue;
     if (epi == EPI_PARTIAL && (ep->split_k < 1 || K % (ep->split_k * GEMM_BK) != 0)) return hipErrorInvalidValue;
-    const bf16_t* a = reinterpret_cast<const bf16_t*>(A);
-    const bf16_t* w = reinterpret_cast<const bf16_t*>(W);
     switch (epi) {
-        case EPI_BF16: return launch_gemm_epi<EPI_BF16>(a, lda, w, ldw, M, N, K, *ep, stream);
-        case EPI_GELU_TANH: return launch_gemm_epi<EPI_GELU_TANH>(a, lda, w, ldw, M, N, K, *ep, stream);
-        case EPI_GELU_ERF: return launch_gemm_epi<EPI_GELU_ERF>(a, lda, w, ldw, M, N, K, *ep, stream);
-        case EPI_F32: return launch_gemm_epi<EPI_F32>(a, lda, w, ldw, M, N, K, *ep, stream);
-        case EPI_QKV: return launch_gemm_epi<EPI_QKV>(a, lda, w, ldw, M, N, K, *ep, stream);
-        case EPI_ARGMAX: return launch_gemm_epi<EPI_ARGMAX>(a, lda, w, ldw, M, N, K, *ep, stream);
-        case EPI_PARTIAL: return launch_gemm_epi<EPI_PARTIAL>(a, lda, w, ldw, M, N, K, *ep, stream);
+        case EPI_BF16: return launch_gemm_epi<EPI_BF16, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_GELU_TANH: return launch_gemm_epi<EPI_GELU_TANH, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_GELU_ERF: return launch_gemm_epi<EPI_GELU_ERF, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_F32: return launch_gemm_epi<EPI_F32, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_QKV: return launch_gemm_epi<EPI_QKV, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_ARGMAX: return launch_gemm_epi<EPI_ARGMAX, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_PARTIAL: return launch_gemm_epi<EPI_PARTIAL, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// W8A8 fp8 (OCP e4m3) GEMM: A [M][K] and W [N][K] e4m3, ep->a_scale[M] / ep->w_scale[N] fp32.
+// The decode path uses it for the GEMMs fed by a LayerNorm (QKV, c_fc, LM head), whose
+// producer emits the row-scaled fp8 activation directly.
+extern "C" hipError_t dlms_gemm_fp8(int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
+                                    const GemmEpi* ep, hipStream_t stream) {
+    if (K % (2 * GEMM_BK) != 0 || N % 64 != 0 || M <= 0 || !ep->a_scale || !ep->w_scale) return hipErrorInvalidValue;
+    if (epi == EPI_PARTIAL && (ep->split_k < 1 || K % (ep->split_k * 2 * GEMM_BK) != 0)) return hipErrorInvalidValue;
+    switch (epi) {
+        case EPI_BF16: return launch_gemm_epi<EPI_BF16, IN_FP8>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_GELU_TANH: return launch_gemm_epi<EPI_GELU_TANH, IN_FP8>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_QKV: return launch_gemm_epi<EPI_QKV, IN_FP8>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_ARGMAX: return launch_gemm_epi<EPI_ARGMAX, IN_FP8>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_PARTIAL: return launch_gemm_epi<EPI_PARTIAL, IN_FP8>(A, lda, W, ldw, M, N, K, *ep, stream);
         default: return hipErrorInvalidValue;
     }
 }

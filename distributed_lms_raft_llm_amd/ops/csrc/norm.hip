@@ -134,7 +134,9 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
                                                            long long split_stride, const float* __restrict__ bias,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, bf16_t* __restrict__ out,
-                                                           int ldb, int M, int D, float eps, int store_normed) {
+                                                           int ldb, unsigned int* __restrict__ out8, int ld8,
+                                                           float* __restrict__ out8_scale, int M, int D, float eps,
+                                                           int store_normed) {
     const int lane = threadIdx.x;
     const int row = blockIdx.x;
     if (row >= M) return;
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
         for (int i = 0; i < NV4; ++i)
             if (valid[i]) xr[cidx[i]] = v[i];
     }
-    if (out == nullptr && !store_normed) return;
+    if (out == nullptr && out8 == nullptr && !store_normed) return;
     const float mean = wave_sum(s) / (float)D;
     float ss = 0.f;
 #pragma unroll
@@ -202,12 +204,15 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
     const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
     const float4* g4 = reinterpret_cast<const float4*>(gamma);
     const float4* b4 = reinterpret_cast<const float4*>(beta);
+    float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < NV4; ++i) {
         const float4 g = g4[cidx[i]], b = b4[cidx[i]];
         if (valid[i]) {
             const float4 y = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
                                          (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
+            if (out8) v[i] = y;  // kept for the fp8 pass below
             if (out) {
                 uint2 p;
                 p.x = pack_bf16x2(y.x, y.y);
@@ -217,16 +222,63 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
             if (store_normed) xr[cidx[i]] = y;  // post-LN residual stream (BERT): x <- LN(x + ...)
         }
     }
+    if (out8) {  // row-scaled OCP e4m3 copy for the fp8 GEMMs (scale = absmax / 448)
+        amax = wave_max(amax);
+        const float sc = fmaxf(amax, 1e-20f) * (1.f / 448.f);
+        const float inv = 1.f / sc;
+        if (lane == 0) out8_scale[row] = sc;
+#pragma unroll
+        for (int i = 0; i < NV4; ++i) {
+            if (valid[i]) {
+                int w = __builtin_amdgcn_cvt_pk_fp8_f32(v[i].x * inv, v[i].y * inv, 0, false);
+                w = __builtin_amdgcn_cvt_pk_fp8_f32(v[i].z * inv, v[i].w * inv, w, true);
+                out8[(size_t)row * (ld8 >> 2) + cidx[i]] = (unsigned int)w;
+            }
+        }
+    }
+}
+
+// Row-wise fp8 quantisation (prefill / tests): q[r] = e4m3(a[r] / s[r]), s[r] = absmax(a[r]) / 448.
+// One wave per row; bf16 input (the LM-head input of a prefill is a gathered bf16 row).
+__global__ __launch_bounds__(256) void quantize_rows_fp8_kernel(const bf16_t* __restrict__ a, int lda,
+                                                                unsigned int* __restrict__ q, int ldq,
+                                                                float* __restrict__ scale, int M, int D) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= M) return;
+    const bf16_t* ar = a + (size_t)r * lda;
+    float amax = 0.f;
+    for (int c = lane * 4; c < D; c += 256)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fabsf(bf16_to_f32(ar[c + j])));
+    amax = wave_max(amax);
+    const float sc = fmaxf(amax, 1e-20f) * (1.f / 448.f);
+    const float inv = 1.f / sc;
+    if (lane == 0) scale[r] = sc;
+    for (int c = lane * 4; c < D; c += 256) {
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(ar[c]) * inv, bf16_to_f32(ar[c + 1]) * inv, 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(ar[c + 2]) * inv, bf16_to_f32(ar[c + 3]) * inv, w, true);
+        q[(size_t)r * (ldq >> 2) + (c >> 2)] = (unsigned int)w;
+    }
+}
+
+extern "C" hipError_t dlms_quantize_rows_fp8(const void* a, int lda, void* q, int ldq, float* scale, int M, int D,
+                                             hipStream_t stream) {
+    if (D % 4 != 0 || ldq % 4 != 0 || M <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(quantize_rows_fp8_kernel, dim3((M + 3) / 4), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16_t*>(a), lda, reinterpret_cast<unsigned int*>(q), ldq, scale, M, D);
+    return hipGetLastError();
 }
 
 template <int NSPLIT>
 static void launch_add_ln(int nv4, dim3 grid, hipStream_t stream, float* x, int ldx, const float* parts, int ldp,
                           long long split_stride, const float* bias, const float* gamma, const float* beta,
-                          bf16_t* o, int ldb, int M, int D, float eps, int store_normed) {
+                          bf16_t* o, int ldb, unsigned int* o8, int ld8, float* o8s, int M, int D, float eps,
+                          int store_normed) {
 #define ADD_LN_V(V)                                                                                            \
     case V:                                                                                                    \
         hipLaunchKernelGGL((add_layernorm_kernel<NSPLIT, V>), grid, dim3(64), 0, stream, x, ldx, parts, ldp,    \
-                           split_stride, bias, gamma, beta, o, ldb, M, D, eps, store_normed);                  \
+                           split_stride, bias, gamma, beta, o, ldb, o8, ld8, o8s, M, D, eps, store_normed);    \
         break;
     switch (nv4) {
         ADD_LN_V(1) ADD_LN_V(2) ADD_LN_V(3) ADD_LN_V(4) ADD_LN_V(5) ADD_LN_V(6) ADD_LN_V(7) ADD_LN_V(8)
@@ -236,15 +288,15 @@ static void launch_add_ln(int nv4, dim3 grid, hipStream_t stream, float* x, int 
 
 extern "C" hipError_t dlms_add_layernorm(float* x, int ldx, const float* parts, int ldp, long long split_stride,
                                          int nsplit, const float* bias, const float* gamma, const float* beta,
-                                         void* out_bf16, int ldb, int M, int D, float eps, int store_normed,
-                                         hipStream_t stream) {
+                                         void* out_bf16, int ldb, void* out_fp8, int ld8, float* out_fp8_scale,
+                                         int M, int D, float eps, int store_normed, hipStream_t stream) {
     if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0 || nsplit < 0 || nsplit > 8) return hipErrorInvalidValue;
     bf16_t* o = reinterpret_cast<bf16_t*>(out_bf16);
     const int nv4 = (D / 4 + 63) / 64;
 #define ADD_LN_CASE(NS)                                                                                       \
     case NS:                                                                                                  \
-        launch_add_ln<NS>(nv4, dim3(M), stream, x, ldx, parts, ldp, split_stride, bias, gamma, beta, o, ldb, M, D, \
-                          eps, store_normed);                                                                 \
+        launch_add_ln<NS>(nv4, dim3(M), stream, x, ldx, parts, ldp, split_stride, bias, gamma, beta, o, ldb,       \
+                          reinterpret_cast<unsigned int*>(out_fp8), ld8, out_fp8_scale, M, D, eps, store_normed); \
         break;
     switch (nsplit) {
         ADD_LN_CASE(0) ADD_LN_CASE(1) ADD_LN_CASE(2) ADD_LN_CASE(3) ADD_LN_CASE(4) ADD_LN_CASE(5) ADD_LN_CASE(6)

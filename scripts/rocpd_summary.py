@@ -22,3 +22,18 @@ if __name__ == "__main__":
     out.writerow(["kernel", "calls", "total_us", "avg_us", "min_us", "max_us", "pct"])
     for r in rows:
         out.writerow([r[0][:140], r[1]] + [round(x, 2) for x in r[2:]])
+
+
+def gaps(db: str, min_kernels: int = 50):
+    """Idle gaps between consecutive kernels on the busiest queue (graph replays): returns
+    (kernel_count, busy_us, span_us, median_gap_us) over the longest dense stretch."""
+    c = sqlite3.connect(db)
+    rows = c.execute("select start, end from kernels order by start").fetchall()
+    if len(rows) < min_kernels:
+        return None
+    g = [(rows[i + 1][0] - rows[i][1]) / 1e3 for i in range(len(rows) - 1)]
+    dense = [x for x in g if x < 50]  # ignore host gaps between replays / phases
+    dense.sort()
+    busy = sum(e - s for s, e in rows) / 1e3
+    return len(rows), busy, (rows[-1][1] - rows[0][0]) / 1e3, dense[len(dense) // 2] if dense else None, \
+        sum(dense) / max(1, len(dense))

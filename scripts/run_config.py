@@ -83,11 +83,20 @@ class Proc:
             self.p.wait()
 
 
+def progress(msg: str):
+    print(f"[run_config {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def wait_for(pred, timeout: float, what: str, procs=()):
     end = time.time() + timeout
+    t0 = last = time.time()
     while time.time() < end:
         if pred():
+            progress(f"{what}: ready after {time.time() - t0:.1f} s")
             return
+        if time.time() - last > 30:
+            progress(f"waiting for {what} ({time.time() - t0:.0f} s)")
+            last = time.time()
         for p in procs:
             if not p.alive():
                 raise RuntimeError(f"a process died while waiting for {what}: see {p.log.name}")
@@ -142,6 +151,7 @@ def main():
             cmd = [sys.executable] + tut
         tutor = Proc(cmd, os.path.join(work, "tutor.log"), env)
         procs.append(tutor)
+        progress(f"config {args.config}: {cfg} -> {work}")
 
         # ---------------------------------------------------------------- LMS Raft cluster
         servers = {i + 1: f"127.0.0.1:{p}" for i, p in enumerate(lms_ports)}
@@ -227,6 +237,7 @@ def main():
             finally:
                 cl.close()
 
+        progress(f"{args.students} students x {args.queries} queries")
         ths = [threading.Thread(target=student, args=(k,)) for k in range(args.students)]
         for t in ths:
             t.start()
@@ -242,7 +253,10 @@ def main():
             wait_for(lambda: leader() not in (None, old), 30, "re-election")
             failover = {"killed_leader": old, "failover_s": round(time.time() - tk, 3), "new_leader": leader()}
         for t in ths:
-            t.join()
+            while t.is_alive():
+                t.join(timeout=30)
+                if t.is_alive():
+                    progress(f"{len(lat)} answered, {len(errors)} errors so far")
         wall = time.perf_counter() - tq
         inst.close()
 

@@ -247,3 +247,53 @@ def test_add_layernorm_no_update():
     assert torch.equal(x, x0)
     torch.testing.assert_close(out.float(), torch.nn.functional.layer_norm(x0, (768,), g, b, 1e-5), atol=3e-2,
                                rtol=1e-2)
+
+
+# ---------------------------------------------------------------------------- fp8 (W8A8, OCP e4m3)
+def _deq(q, s):
+    return q.float() * s[:, None]
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 2304, 768), (7, 128, 256), (130, 64, 1024)])
+def test_gemm_fp8_matches_dequantized_reference(M, N, K):
+    ops = _ops()
+    a, w = _bf(M, K, seed=31), _bf(N, K, scale=0.05, seed=32)
+    a8, sa = ops.quantize_fp8_rows(a)
+    w8, sw = ops.quantize_fp8_weight(w)
+    # the kernel quantiser agrees with torch's e4m3fn rounding
+    ref8 = (a.float() / sa[:, None]).to(ops.FP8)
+    assert (a8.view(torch.uint8) != ref8.view(torch.uint8)).float().mean() < 1e-3
+    bias = torch.randn(N, device=DEV)
+    out = ops.gemm(a8, w8, ops.EPI_BF16, bias=bias, a_scale=sa, w_scale=sw)
+    ref = _deq(a8, sa) @ _deq(w8, sw).t() + bias
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    # and stays close to the bf16 product it approximates
+    cos = torch.nn.functional.cosine_similarity(out.float().flatten(), (a.float() @ w.float().t() + bias).flatten(),
+                                                dim=0)
+    assert cos > 0.995
+
+
+def test_add_layernorm_fp8_output_and_fp8_argmax():
+    ops = _ops()
+    M, D, V = 33, 768, 4096
+    x = torch.randn(M, D, device=DEV)
+    g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    h8 = torch.empty(M, D, dtype=ops.FP8, device=DEV)
+    hs = torch.empty(M, device=DEV)
+    out = ops.add_layernorm(x, g, b, 1e-5, out_fp8=h8, out_fp8_scale=hs)
+    ref = torch.nn.functional.layer_norm(x, (D,), g, b, 1e-5)
+    torch.testing.assert_close(hs, ref.abs().amax(1) / 448, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(_deq(h8, hs), ref, atol=0.08 * ref.abs().amax().item() / 8, rtol=0.07)
+    assert out is not None
+    # fp8 LM head with the fused penalty + argmax epilogue equals argmax of the dequantised logits
+    w8, sw = ops.quantize_fp8_weight(_bf(V, D, scale=0.05, seed=33))
+    keys = torch.zeros(M, V // 64, dtype=torch.int64, device=DEV)
+    seen = torch.zeros(M, V // 32, dtype=torch.int32, device=DEV)
+    ops.gemm(h8, w8, ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V - 5, penalty=1.2, a_scale=hs, w_scale=sw)
+    logits = _deq(h8, hs) @ _deq(w8, sw).t()
+    logits[:, V - 5:] = float("-inf")
+    red = ops.argmax_reduce(keys)  # unsigned key max on the device
+    idx = (~(red & 0xFFFFFFFF)) & 0xFFFFFFFF
+    top2 = logits.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-3  # ignore near-ties (fp32 summation order)
+    assert torch.equal(idx[clear], logits.argmax(1)[clear])
