@@ -84,7 +84,9 @@ def _bucket(n: int) -> int:
 class HipGPT2Engine:
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
-                 check_every: int = 16, max_batch_cap: int = 4096):
+                 check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16"):
+        """``weight_dtype="fp8"``: W8A8 OCP-e4m3 MFMA GEMMs for QKV, c_fc and the LM head (activation
+        rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path."""
         if not torch.cuda.is_available():
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
@@ -100,7 +102,10 @@ class HipGPT2Engine:
         if isinstance(weights, GPT2DeviceWeights):
             self.w = weights
         else:
-            self.w = prepare_gpt2_weights(cfg, weights, self.device, self.tp_rank, self.tp_size)
+            if weight_dtype not in ("bf16", "fp8"):
+                raise ValueError(f"weight_dtype {weight_dtype!r}: bf16 or fp8")
+            self.w = prepare_gpt2_weights(cfg, weights, self.device, self.tp_rank, self.tp_size,
+                                          fp8=weight_dtype == "fp8")
         if max_length > cfg.n_positions:
             raise ValueError("max_length exceeds n_positions")
         if not max_batch or max_batch == "auto":  # size the slot pool from free HBM (engine/memory.py)
@@ -129,6 +134,10 @@ class HipGPT2Engine:
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.att = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.ff = torch.zeros(B, Fl, dtype=bf, device=dev)
+        self.h8 = self.hsc = None
+        if self.w.fp8:  # row-scaled e4m3 LayerNorm outputs (K zero-padded to the fp8 ring step)
+            self.h8 = torch.zeros(B, self.w.k_fp8, dtype=ops.FP8, device=dev)
+            self.hsc = torch.ones(B, dtype=f32, device=dev)
         # LM-head argmax partial keys: one per (row, 64-column group) of this rank's vocab shard;
         # zero-initialised once (columns a 128-wide tile never writes stay at the minimum key)
         self.key_parts = torch.zeros(B, self.w.lm_head.shape[0] // 64, dtype=torch.int64, device=dev)
@@ -204,39 +213,72 @@ class HipGPT2Engine:
         return parts, s, bias
 
     def _layers(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
-                final_h: torch.Tensor | None):
+                final_h: torch.Tensor | None, h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None):
         """All blocks on rows [0, M) of the residual ``x`` (updated in place), then ln_f into
-        ``final_h`` (or only the last residual update when ``final_h`` is None)."""
+        ``final_h`` (or only the last residual update when ``final_h`` is None).  fp8 weights: the
+        LayerNorms emit row-scaled e4m3 into ``h8``/``hsc`` for the W8A8 QKV / c_fc GEMMs, and the
+        ln_f output goes there too (``final_h`` then only says whether it is wanted)."""
         w, cfg = self.w, self.cfg
         eps = cfg.layer_norm_epsilon
         xs, hs, qs, ats, ffs = x[:M], h[:M], q[:M], att[:M], ff[:M]
+        fp8 = w.fp8
+        ln_out = dict(out_bf16=None, want_out=False, out_fp8=h8[:M] if fp8 else None,
+                      out_fp8_scale=hsc[:M] if fp8 else None) if fp8 else dict(out_bf16=hs)
         pend = (None, 0, None)
         for li, lw in enumerate(w.layers):
             kc, vc = self.kv[li, 0], self.kv[li, 1]
-            ops.add_layernorm(xs, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], out_bf16=hs)
-            ops.gemm(hs, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
-                     row_slot=row_slot, row_pos=row_pos)
+            ops.add_layernorm(xs, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **ln_out)
+            if fp8:
+                ops.gemm(h8[:M], lw.w_qkv8, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
+                         row_slot=row_slot, row_pos=row_pos, a_scale=hsc[:M], w_scale=lw.s_qkv)
+            else:
+                ops.gemm(hs, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
+                         row_slot=row_slot, row_pos=row_pos)
             ops.row_attention(qs, kc, vc, row_slot, row_kvlen, out=ats)
             pend = self._row_parallel(ats, lw.w_o, lw.b_o, parts, M)
-            ops.add_layernorm(xs, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], out_bf16=hs)
-            ops.gemm(hs, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs)
+            ops.add_layernorm(xs, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **ln_out)
+            if fp8:
+                ops.gemm(h8[:M], lw.w_fc8, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs, a_scale=hsc[:M], w_scale=lw.s_fc)
+            else:
+                ops.gemm(hs, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs)
             pend = self._row_parallel(ffs, lw.w_p, lw.b_p, parts, M)
-        ops.add_layernorm(xs, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], out_bf16=final_h,
-                          want_out=final_h is not None)
+        if fp8:
+            fin = ln_out if final_h is not None else dict(want_out=False)
+            ops.add_layernorm(xs, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **fin)
+        else:
+            ops.add_layernorm(xs, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2],
+                              out_bf16=final_h, want_out=final_h is not None)
 
-    def _lm_head_and_update(self, hidden_bf16: torch.Tensor, B: int, penalty: float):
+    def _lm_head_and_update(self, hidden: torch.Tensor, B: int, penalty: float, seen: torch.Tensor | None = None,
+                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None):
+        """LM head with the fused penalty + argmax on ``hidden`` (bf16, or e4m3 with ``hscale``),
+        then the greedy bookkeeping.  Rows map to slots [0, B) or through ``slot_map``."""
         cfg = self.cfg
-        ops.gemm(hidden_bf16, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[:B], seen=self.seen[:B],
-                 vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
+        seen_rows = self.seen[:B] if seen is None else seen
+        if hidden.dtype == ops.FP8:
+            ops.gemm(hidden, self.w.lm_head8, ops.EPI_ARGMAX, argmax_out=self.key_parts[:B], seen=seen_rows,
+                     vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty, a_scale=hscale,
+                     w_scale=self.w.s_lm)
+        else:
+            ops.gemm(hidden, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[:B], seen=seen_rows,
+                     vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
         keys = self._gather_keys(B)
-        ops.decode_update(keys, self.lens[:B], self.finished[:B], self.out_tokens[:B],
-                          self.seen[:B], self.cur_tok[:B], self.cur_pos[:B], self.cur_kvlen[:B], self.w.wte,
-                          self.w.wpe, self.x[:B], cfg.eos_token_id, self.max_length)
+        if slot_map is None:
+            ops.decode_update(keys, self.lens[:B], self.finished[:B], self.out_tokens[:B],
+                              self.seen[:B], self.cur_tok[:B], self.cur_pos[:B], self.cur_kvlen[:B], self.w.wte,
+                              self.w.wpe, self.x[:B], cfg.eos_token_id, self.max_length)
+        else:
+            ops.decode_update(keys, self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
+                              self.cur_kvlen, self.w.wte, self.w.wpe, self.x, cfg.eos_token_id, self.max_length,
+                              slot_map=slot_map)
 
     def _decode_step(self, B: int, penalty: float):
         self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
-                     self.cur_kvlen[:B], B, final_h=self.h[:B])
-        self._lm_head_and_update(self.h[:B], B, penalty)
+                     self.cur_kvlen[:B], B, final_h=self.h[:B], h8=self.h8, hsc=self.hsc)
+        if self.w.fp8:
+            self._lm_head_and_update(self.h8[:B], B, penalty, hscale=self.hsc[:B])
+        else:
+            self._lm_head_and_update(self.h[:B], B, penalty)
 
     def _graph_for(self, B: int, penalty: float) -> torch.cuda.CUDAGraph:
         key = (B, float(penalty))
@@ -325,14 +367,19 @@ class HipGPT2Engine:
         q = torch.empty(R, Dl, dtype=bf, device=dev)
         att = torch.empty(R, Dl, dtype=bf, device=dev)
         ff = torch.empty(R, Fl, dtype=bf, device=dev)
-        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None)
+        h8 = hsc = None
+        if self.w.fp8:
+            h8 = torch.zeros(R, self.w.k_fp8, dtype=ops.FP8, device=dev)  # K padding stays zero
+            hsc = torch.empty(R, dtype=f32, device=dev)
+        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None, h8=h8, hsc=hsc)
         hl = ops.layernorm_gather(x, last_d, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon)
+        hsc_l = None
+        if self.w.fp8:
+            hl8 = torch.zeros(n, self.w.k_fp8, dtype=ops.FP8, device=dev)  # K padding stays zero
+            _, hsc_l = ops.quantize_fp8_rows(hl, out=hl8)
+            hl = hl8
         # first token: argmax rows are prompts (seen rows gathered), updates land in their slots
-        ops.gemm(hl, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[:n], seen=seen_d,
-                 vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
-        keys = self._gather_keys(n)
-        ops.decode_update(keys, self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
-                          self.cur_kvlen, self.w.wte, self.w.wpe, self.x, cfg.eos_token_id, T, slot_map=slots_d)
+        self._lm_head_and_update(hl, n, penalty, seen=seen_d, hscale=hsc_l, slot_map=slots_d)
 
     def _prefill(self, prompts: list[list[int]], B: int, penalty: float):
         """Static batch: prompts into slots [0, n), slots [n, B) inert."""
@@ -355,7 +402,11 @@ class HipGPT2Engine:
         parts = torch.empty(nsplit, R, D, device=dev)
         bf = torch.bfloat16
         h, q, att, ff = (torch.empty(R, n, dtype=bf, device=dev) for n in (D, Dl, Dl, Fl))
-        self._layers(x, parts, h, q, att, ff, slot, pos, pos + 1, R, final_h=None)
+        h8 = hsc = None
+        if self.w.fp8:
+            h8 = torch.zeros(R, self.w.k_fp8, dtype=ops.FP8, device=dev)
+            hsc = torch.empty(R, device=dev)
+        self._layers(x, parts, h, q, att, ff, slot, pos, pos + 1, R, final_h=None, h8=h8, hsc=hsc)
         return ops.layernorm_gather(x, last, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon).float()
 
     # ------------------------------------------------------------------ slot API (continuous batching)

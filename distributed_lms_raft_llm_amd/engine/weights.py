@@ -48,6 +48,12 @@ class LayerWeights:
     b_fc: torch.Tensor  # [Fl]
     w_p: torch.Tensor  # [D, Fl]
     b_p: torch.Tensor  # [D], added once after the reduction
+    # fp8 (W8A8) copies of the LayerNorm-fed GEMMs: e4m3 [N, Kp] (K zero-padded to a multiple of
+    # 128) + per-output-channel f32 scales; None for the bf16 engine
+    w_qkv8: torch.Tensor | None = None
+    s_qkv: torch.Tensor | None = None
+    w_fc8: torch.Tensor | None = None
+    s_fc: torch.Tensor | None = None
 
 
 @dataclass
@@ -63,6 +69,17 @@ class GPT2DeviceWeights:
     lnf_g: torch.Tensor
     lnf_b: torch.Tensor
     layers: list[LayerWeights] = field(default_factory=list)
+    lm_head8: torch.Tensor | None = None  # fp8 LM-head shard [V1-V0, Kp] + scales
+    s_lm: torch.Tensor | None = None
+
+    @property
+    def fp8(self) -> bool:
+        return self.lm_head8 is not None
+
+    @property
+    def k_fp8(self) -> int:
+        """K of the fp8 GEMMs: d padded to the fp8 kernel's 128-element ring step."""
+        return -(-self.cfg.n_embd // 128) * 128
 
     @property
     def n_heads_local(self) -> int:
@@ -88,8 +105,20 @@ class GPT2DeviceWeights:
         return n
 
 
+def quantize_fp8_padded(w: torch.Tensor, kp: int):
+    """[N, K] -> (e4m3 [N, kp] zero-padded, f32 per-row scales): scale = absmax / 448."""
+    wf = w.float()
+    scale = wf.abs().amax(dim=1).clamp_min(1e-20) / 448.0
+    q = torch.zeros(wf.shape[0], kp, dtype=torch.float8_e4m3fn, device=wf.device)
+    q[:, : wf.shape[1]] = (wf / scale[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    return q, scale.contiguous()
+
+
 def prepare_gpt2_weights(cfg: GPT2Config, w: dict[str, torch.Tensor], device, tp_rank: int = 0, tp_size: int = 1,
-                         dtype=torch.bfloat16) -> GPT2DeviceWeights:
+                         dtype=torch.bfloat16, fp8: bool = False) -> GPT2DeviceWeights:
+    """Shard + lay out GPT-2 weights for this TP rank.  ``fp8``: additionally quantise the QKV,
+    c_fc and LM-head weights to OCP e4m3 with per-output-channel scales (the W8A8 path; the
+    row-parallel out-proj / c_proj, whose inputs have no cheap row scale, stay bf16)."""
     D, H, hd = cfg.n_embd, cfg.n_head, cfg.head_dim
     assert hd == 64, "kernels assume 64-wide heads (all GPT-2 sizes)"
     h0, h1 = shard_range(H, tp_size, tp_rank)
@@ -131,4 +160,10 @@ def prepare_gpt2_weights(cfg: GPT2Config, w: dict[str, torch.Tensor], device, tp
             w_fc=dev(wfc), b_fc=dev(w[p + "mlp.c_fc.bias"].float()[f0:f1], f32),
             w_p=dev(wp), b_p=dev(w[p + "mlp.c_proj.bias"], f32),
         ))
+    if fp8:
+        kp = out.k_fp8
+        for lw in out.layers:
+            lw.w_qkv8, lw.s_qkv = quantize_fp8_padded(lw.w_qkv, kp)
+            lw.w_fc8, lw.s_fc = quantize_fp8_padded(lw.w_fc, kp)
+        out.lm_head8, out.s_lm = quantize_fp8_padded(out.lm_head, kp)
     return out

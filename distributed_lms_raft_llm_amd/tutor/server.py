@@ -133,7 +133,7 @@ class TutoringServicer:
 
 
 def make_engine(model: str, device: str, max_batch: int, max_length: int, weights: str | None = None, seed: int = 0,
-                tp_group=None):
+                tp_group=None, weight_dtype: str = "bf16"):
     """GPU: the HIP engine (TP over ``tp_group`` when given).  CPU: the torch reference engine, or
     the sharded torch slot engine when a (gloo) TP group is given."""
     cfg = gpt2_config(model)
@@ -143,7 +143,8 @@ def make_engine(model: str, device: str, max_batch: int, max_length: int, weight
     if device.startswith("cuda"):
         from ..engine.gpt2_engine import HipGPT2Engine
 
-        return HipGPT2Engine(cfg, w, device=device, max_batch=max_batch, max_length=max_length, tp_group=tp_group)
+        return HipGPT2Engine(cfg, w, device=device, max_batch=max_batch, max_length=max_length, tp_group=tp_group,
+                             weight_dtype=weight_dtype)
     if tp_group is not None:
         from ..parallel.tp import TorchSlotEngine
 
@@ -214,6 +215,8 @@ def main(argv=None):
     ap.add_argument("--window-ms", type=float, default=2.0)
     ap.add_argument("--max-length", type=int, default=150)
     ap.add_argument("--repetition-penalty", type=float, default=1.2)
+    ap.add_argument("--weight-dtype", choices=("bf16", "fp8"), default="bf16",
+                    help="fp8: W8A8 e4m3 MFMA GEMMs for QKV / c_fc / LM head (GPU engine)")
     ap.add_argument("--tp", type=int, default=0, help="tensor-parallel degree under torchrun (default: world)")
     ap.add_argument("--batching", choices=("auto", "continuous", "window"), default="auto")
     ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
@@ -240,7 +243,8 @@ def main(argv=None):
                 ctrl = grp
         src = dp_idx * tp
         device = f"cuda:{local}" if args.device != "cpu" and torch.cuda.is_available() else "cpu"
-        eng = make_engine(args.model, device, args.max_batch, args.max_length, args.weights, tp_group=tp_group)
+        eng = make_engine(args.model, device, args.max_batch, args.max_length, args.weights, tp_group=tp_group,
+                          weight_dtype=args.weight_dtype)
         if rank != src:
             n = serve_follower(eng, ctrl, src)
             log.info("TP follower rank %d done after %d commands", rank, n)
@@ -248,7 +252,8 @@ def main(argv=None):
         proxy = eng = TPEngineProxy(eng, ctrl, src)
         args.port += dp_idx
     else:
-        eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights)
+        eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights,
+                          weight_dtype=args.weight_dtype)
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,

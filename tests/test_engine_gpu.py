@@ -108,3 +108,22 @@ def test_continuous_batching_matches_static():
             agree = sum(int(a == b) for a, b in zip(g_[len(p): n], r_[len(p): n]))
             assert agree >= 0.5 * (n - len(p)), (g_, r_)
     assert cb.completed == len(prompts)
+
+
+def test_fp8_engine_tracks_bf16():
+    """W8A8 e4m3 engine (QKV, c_fc, LM head on the fp8 MFMA path): last-token hidden states stay
+    close to the bf16 engine's and greedy decode agrees on the first tokens."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [12, 30, 5], seed=7)
+    e16 = HipGPT2Engine(cfg, w, max_batch=4, max_length=48)
+    e8 = HipGPT2Engine(cfg, w, max_batch=4, max_length=48, weight_dtype="fp8")
+    assert e8.w.fp8 and e8.w.layers[0].w_qkv8 is not None
+    h16, h8 = e16.prefill_last_hidden(prompts), e8.prefill_last_hidden(prompts)
+    for a, b in zip(h16, h8):
+        assert torch.nn.functional.cosine_similarity(a, b, dim=0).item() > 0.99
+    g16, g8 = e16.generate(prompts), e8.generate(prompts)
+    for a, b, p in zip(g16, g8, prompts):
+        assert b[: len(p)] == p and len(b) <= 48
+        assert a[len(p)] == b[len(p)]
