@@ -91,7 +91,9 @@ class HipGPT2Engine:
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
         self.cfg = cfg
-        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:  # pin "cuda" to a concrete ordinal (scheduler threads set it)
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.tp_group = tp_group
         if tp_group is not None:
             import torch.distributed as dist

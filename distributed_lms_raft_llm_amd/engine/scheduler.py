@@ -92,10 +92,10 @@ class ContinuousBatcher:
 
     # ------------------------------------------------------------------ scheduler thread
     def _run(self):
-        dev = getattr(self.engine, "device", None)
-        if dev is not None and getattr(dev, "type", None) == "cuda":
-            torch.cuda.set_device(dev)
         try:
+            dev = getattr(self.engine, "device", None)
+            if dev is not None and getattr(dev, "type", None) == "cuda" and dev.index is not None:
+                torch.cuda.set_device(dev)
             with torch.no_grad():
                 self._loop()
         except BaseException as e:  # fail every waiter loudly instead of hanging them

@@ -59,6 +59,7 @@ def main():
                     help="rotate GEMM weights over >= this many MB per graph so they stream from HBM like "
                          "the 12-layer decode step (0: one L2/MALL-hot weight)")
     ap.add_argument("--ops", default="qkv,oproj,fc,proj,lmhead,attn,add_ln")
+    ap.add_argument("--vendor", action="store_true", help="also time torch.mm (hipBLASLt) on the same shapes")
     args = ap.parse_args()
     ops_on = set(args.ops.split(","))
     L = ops.lib()
@@ -107,8 +108,10 @@ def main():
                                                                    seen=seen, vocab=50257, penalty=1.2)))
             else:
                 variants.append(("bf16", lambda i, x=x, N=N: ops.gemm(x, ws[i % nw], ops.EPI_BF16, out=out_bf[:, :N])))
+            if args.vendor:  # hipBLASLt/rocBLAS via torch, same shapes and weight rotation (reference point)
+                variants.append(("torch_mm", lambda i, x=x: torch.mm(x, ws[i % nw].t())))
             for vname, fn in variants:
-                for t in tiles:
+                for t in (tiles if vname != "torch_mm" else [-1]):
                     L.dlms_gemm_force_tile(t)
                     try:
                         med, mn = graph_time(fn, inner=inner)
