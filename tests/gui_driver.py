@@ -16,6 +16,8 @@ def main():
     ref_dir, addr_map, workdir = sys.argv[1], json.loads(sys.argv[2]), sys.argv[3]
     sys.path.insert(0, os.path.join(HERE, "fake_tk"))
     sys.path.insert(0, ref_dir)
+    if os.environ.get("GUI_OWN_STUBS") == "1":  # this framework's lms_pb2 / lms_pb2_grpc, not protoc's
+        sys.path.insert(0, os.path.dirname(HERE))
     import grpc
 
     real = grpc.insecure_channel
@@ -28,8 +30,11 @@ def main():
     from tkinter import filedialog, messagebox
 
     import lms_gui_final as gui
+    import lms_pb2
 
-    out = {"steps": []}
+    out_stub_origin = lms_pb2.__file__
+
+    out = {"steps": [], "stubs": out_stub_origin}
 
     def click(text, idx=-1):
         bs = tk.find_buttons(text)

@@ -19,7 +19,10 @@ pytestmark = [pytest.mark.timeout(180),
                                  reason="reference GUI not mounted")]
 
 
-def test_reference_gui_runs_unchanged_against_cluster(tmp_path):
+@pytest.mark.parametrize("stubs", ["reference", "ours"])
+def test_reference_gui_runs_unchanged_against_cluster(tmp_path, stubs):
+    """``stubs="ours"``: the GUI imports this framework's lms_pb2 / lms_pb2_grpc (runtime-built
+    drop-ins), so a user needs nothing from the reference but the GUI file itself."""
     tsrv, tport, tutor = start_tutor()
     from lms_harness import KeywordGate
 
@@ -30,6 +33,7 @@ def test_reference_gui_runs_unchanged_against_cluster(tmp_path):
         env = dict(os.environ)
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+        env["GUI_OWN_STUBS"] = "1" if stubs == "ours" else "0"
         p = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gui_driver.py"), REF,
                             json.dumps(amap), str(tmp_path)], capture_output=True, text=True, timeout=150, env=env)
         line = [ln for ln in p.stdout.splitlines() if ln.startswith("GUI_RESULT ")]
@@ -38,6 +42,8 @@ def test_reference_gui_runs_unchanged_against_cluster(tmp_path):
     finally:
         c.close()
         tsrv.stop(0)
+    own = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert res["stubs"].startswith(own if stubs == "ours" else REF), res["stubs"]
     steps = {s[0] + (("/" + s[1]) if s[0] in ("register", "login") else ""): s for s in res["steps"]}
     assert steps["register/stud"][2] == ["info", "Registration Success",
                                          "Registration request is being processed. Please wait."]

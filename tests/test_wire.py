@@ -129,3 +129,43 @@ def test_unimplemented_methods_answer_unimplemented(tmp_path):
         ch.close()
     finally:
         c.close()
+
+
+def test_dropin_generated_modules():
+    """Top-level lms_pb2 / lms_pb2_grpc: the generated modules' API (stubs, servicer bases with
+    UNIMPLEMENTED defaults, add_*_to_server, experimental static calls)."""
+    import importlib.util
+    from concurrent import futures
+
+    import grpc
+
+    from distributed_lms_raft_llm_amd.wire import lms_pb2, lms_pb2_grpc
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for name in ("lms_pb2", "lms_pb2_grpc"):  # the top-level shims re-export them (loaded by path:
+        spec = importlib.util.spec_from_file_location(f"_shim_{name}", os.path.join(root, f"{name}.py"))
+        mod = importlib.util.module_from_spec(spec)  # another test may have cached the reference's)
+        spec.loader.exec_module(mod)
+        assert hasattr(mod, "LoginRequest" if name == "lms_pb2" else "LMSStub")
+    assert lms_pb2.DESCRIPTOR.package == "lms"
+
+    class Tutor(lms_pb2_grpc.Tutoring):  # the reference tutoring server subclasses this class
+        def GetLLMAnswer(self, request, context):
+            return lms_pb2.QueryResponse(success=True, response="echo " + request.query)
+
+    srv = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+    lms_pb2_grpc.add_TutoringServicer_to_server(Tutor(), srv)
+    lms_pb2_grpc.add_RaftServiceServicer_to_server(lms_pb2_grpc.RaftServiceServicer(), srv)
+    port = srv.add_insecure_port("127.0.0.1:0")
+    srv.start()
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+            r = lms_pb2_grpc.TutoringStub(ch).GetLLMAnswer(lms_pb2.QueryRequest(token="t", query="q"), timeout=5)
+            assert r.success and r.response == "echo q"
+            with pytest.raises(grpc.RpcError) as e:
+                lms_pb2_grpc.RaftServiceStub(ch).WhoIsLeader(lms_pb2.Empty(), timeout=5)
+            assert e.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        r = lms_pb2_grpc.Tutoring.GetLLMAnswer(lms_pb2.QueryRequest(query="s"), f"127.0.0.1:{port}", timeout=5)
+        assert r.response == "echo s"
+    finally:
+        srv.stop(0)
