@@ -358,6 +358,10 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
             case 8: return launch_gemm_cfg<256, 128, 4, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             case 10: return launch_gemm_cfg<128, 128, 4, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             case 11: return launch_gemm_cfg<128, 128, 2, 4, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            // big per-wave tiles (128x64 per wave): more MFMA work per LDS byte read (64x64 wave
+            // tiles sit exactly at the CU's LDS-bandwidth : MFMA-rate balance)
+            case 12: return launch_gemm_cfg<256, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 13: return launch_gemm_cfg<256, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             default: break;
         }
     }
