@@ -37,6 +37,7 @@ class _Req:
     prompt: list[int]
     future: Future
     t_submit: float = field(default_factory=time.perf_counter)
+    t_first: float = 0.0
 
 
 class ContinuousBatcher:
@@ -131,9 +132,12 @@ class ContinuousBatcher:
                     eng.admit([r.prompt for _, r in admits], [s for s, _ in admits], self.penalty)
                 TRACER.complete("tutor.admit", ta, cat="tutor", n=len(admits),
                                 tokens=sum(len(r.prompt) for _, r in admits))
+                t_first = time.perf_counter()  # prefill emitted every admitted query's first token
                 for s, r in admits:
                     self._active[s] = r
-                    METRICS.observe(f"{self.name}_queue_ms", (time.perf_counter() - r.t_submit) * 1e3)
+                    r.t_first = t_first
+                    METRICS.observe(f"{self.name}_queue_ms", (ta - r.t_submit) * 1e3)
+                    METRICS.observe(f"{self.name}_ttft_ms", (t_first - r.t_submit) * 1e3)
             B = min(_bucket(max(self._active) + 1), eng.max_batch)
             td = time.perf_counter()
             with roctx_range("decode_chunk"):
@@ -152,7 +156,11 @@ class ContinuousBatcher:
                     r = self._active.pop(s)
                     heapq.heappush(self._free, s)
                     self.completed += 1
+                    n_new = len(out) - len(r.prompt)
                     METRICS.observe(f"{self.name}_request_ms", (now - r.t_submit) * 1e3)
-                    METRICS.inc(f"{self.name}_tokens", len(out) - len(r.prompt))
+                    if n_new > 1:  # time per output token after the first
+                        METRICS.observe(f"{self.name}_tpot_ms", (now - r.t_first) * 1e3 / (n_new - 1))
+                    METRICS.inc(f"{self.name}_tokens", n_new)
                     r.future.set_result(out)
             METRICS.set(f"{self.name}_active", len(self._active))
+            METRICS.set(f"{self.name}_kv_slot_occupancy", len(self._active) / eng.max_batch)

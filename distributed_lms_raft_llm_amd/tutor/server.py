@@ -185,6 +185,12 @@ class TutoringServer:
         b = self.batcher
         out = {"batching": self.batching, "engine": type(getattr(self.engine, "engine", self.engine)).__name__,
                "max_length": self.gen.max_length}
+        eng = getattr(self.engine, "engine", self.engine)
+        if getattr(eng, "device", None) is not None and eng.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(eng.device)
+            out.update(hbm_used_gb=round((total - free) / 2**30, 2), hbm_total_gb=round(total / 2**30, 2),
+                       kv_cache_gb=round(eng.kv_cache_bytes() / 2**30, 3), slots=eng.max_batch)
+            METRICS.set("tutor_hbm_used_gb", out["hbm_used_gb"])
         if self.batching == "continuous":
             out.update(active=b.active, completed=b.completed, ok=b._error is None and b._thread.is_alive())
         else:

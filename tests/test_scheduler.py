@@ -97,6 +97,11 @@ def test_outputs_match_solo_runs_with_staggered_arrivals():
         cb.stop()
     assert outs == [solo(p, 40) for p in prompts]
     assert cb.completed == 23
+    from distributed_lms_raft_llm_amd.utils.metrics import METRICS
+
+    h = METRICS.snapshot()["histograms"]
+    assert h["tutor_ttft_ms"]["count"] >= 23 and h["tutor_tpot_ms"]["count"] > 0
+    assert 0.0 <= METRICS.snapshot()["gauges"]["tutor_kv_slot_occupancy"] <= 1.0
     assert eng.admitted_while_busy > 0  # requests joined a running batch
     assert max(eng.buckets) <= 4
 
