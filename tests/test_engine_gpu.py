@@ -24,8 +24,9 @@ def _prompts(cfg, lens, seed=1):
     return [torch.randint(0, cfg.vocab_size - 1, (L,), generator=g).tolist() for L in lens]
 
 
-@pytest.mark.parametrize("name", ["gpt2-tiny", "gpt2"])
+@pytest.mark.parametrize("name", ["gpt2-tiny", "gpt2", "gpt2-medium", "gpt2-xl"])
 def test_prefill_hidden_matches_reference(name):
+    """gpt2-xl: 25 heads, d = 1600 (not a multiple of 256/128: ragged LayerNorm lanes, fp8 K pad)."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
     from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, KVCache
 
@@ -113,17 +114,27 @@ def test_continuous_batching_matches_static():
 def test_fp8_engine_tracks_bf16():
     """W8A8 e4m3 engine (QKV, c_fc, LM head on the fp8 MFMA path): last-token hidden states stay
     close to the bf16 engine's and greedy decode agrees on the first tokens."""
-    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
-
     cfg, w = _setup("gpt2")
     prompts = _prompts(cfg, [12, 30, 5], seed=7)
+    _fp8_vs_bf16(cfg, w, prompts)
+
+
+def test_fp8_engine_tracks_bf16_xl():
+    cfg, w = _setup("gpt2-xl")
+    _fp8_vs_bf16(cfg, w, _prompts(cfg, [12, 3], seed=8), first_token=False, min_cos=0.97)
+
+
+def _fp8_vs_bf16(cfg, w, prompts, first_token=True, min_cos=0.99):
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
     e16 = HipGPT2Engine(cfg, w, max_batch=4, max_length=48)
     e8 = HipGPT2Engine(cfg, w, max_batch=4, max_length=48, weight_dtype="fp8")
     assert e8.w.fp8 and e8.w.layers[0].w_qkv8 is not None
     h16, h8 = e16.prefill_last_hidden(prompts), e8.prefill_last_hidden(prompts)
     for a, b in zip(h16, h8):
-        assert torch.nn.functional.cosine_similarity(a, b, dim=0).item() > 0.99
+        assert torch.nn.functional.cosine_similarity(a, b, dim=0).item() > min_cos
     g16, g8 = e16.generate(prompts), e8.generate(prompts)
     for a, b, p in zip(g16, g8, prompts):
         assert b[: len(p)] == p and len(b) <= 48
-        assert a[len(p)] == b[len(p)]
+        if first_token:
+            assert a[len(p)] == b[len(p)]
