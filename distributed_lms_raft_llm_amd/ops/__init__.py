@@ -108,6 +108,8 @@ def _bind(L):
         fn.restype = ctypes.c_int
     L.dlms_gemm_force_tile.argtypes = [ctypes.c_int]
     L.dlms_gemm_force_tile.restype = None
+    L.dlms_attention_variant.argtypes = [ctypes.c_int]
+    L.dlms_attention_variant.restype = None
     L.dlms_error_string.argtypes = [ctypes.c_int]
     L.dlms_error_string.restype = ctypes.c_char_p
     L.dlms_gemm_epi_size.restype = ctypes.c_int

@@ -110,8 +110,8 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
 // in registers (exp2 with log2(e) folded into q), ATT_UNROLL key-steps of K and V loads issued
 // before any use, then a shuffle merge of the 8 per-group (max, sum, acc) triples.  No LDS, no
 // barriers: the kernel is a pure KV stream.
-#define ATT_UNROLL 4
-
+// NT: non-temporal K/V loads (the cache is streamed once per step; keep L2/MALL for weights).
+template <int ATT_UNROLL, bool NT>
 __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict__ q, int ldq,
                                                         const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                                         const int* __restrict__ row_slot,
@@ -143,8 +143,16 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
         for (int u = 0; u < ATT_UNROLL; ++u) {
             int t = t0 + u * 8 + g;
             t = t < kvlen ? t : kvlen - 1;  // clamped (masked below): loads never leave the slot
-            kr[u] = *reinterpret_cast<const uint4*>(K + (size_t)t * 64);
-            vr[u] = *reinterpret_cast<const uint4*>(V + (size_t)t * 64);
+            if constexpr (NT) {
+                typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+                const u32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(K + (size_t)t * 64));
+                const u32x4_t b = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(V + (size_t)t * 64));
+                kr[u] = make_uint4(a.x, a.y, a.z, a.w);
+                vr[u] = make_uint4(b.x, b.y, b.z, b.w);
+            } else {
+                kr[u] = *reinterpret_cast<const uint4*>(K + (size_t)t * 64);
+                vr[u] = *reinterpret_cast<const uint4*>(V + (size_t)t * 64);
+            }
         }
 #pragma unroll
         for (int u = 0; u < ATT_UNROLL; ++u) {
@@ -195,14 +203,25 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
     }
 }
 
+static int g_attn_variant = 0;  // tuning override: 0 = (unroll 4), 1 = (8), 2 = (4, nt), 3 = (8, nt)
+extern "C" void dlms_attention_variant(int v) { g_attn_variant = v; }
+
 extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                      const int* row_kvlen, void* out, int ldo, int R, int H, int t_max, float scale,
                                      hipStream_t stream) {
     if (R <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
     const float scale_log2 = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_wave_kernel, dim3((H + 3) / 4, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q),
-                       ldq, reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
-                       row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale_log2);
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((H + 3) / 4, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
+                           reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
+                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale_log2);
+    };
+    switch (g_attn_variant) {
+        case 1: launch(attn_wave_kernel<8, false>); break;
+        case 2: launch(attn_wave_kernel<4, true>); break;
+        case 3: launch(attn_wave_kernel<8, true>); break;
+        default: launch(attn_wave_kernel<4, false>); break;
+    }
     return hipGetLastError();
 }
 
