@@ -110,6 +110,11 @@ def _bind(L):
     L.dlms_gemm_force_tile.restype = None
     L.dlms_attention_variant.argtypes = [ctypes.c_int]
     L.dlms_attention_variant.restype = None
+    # in-situ tuning knobs (tests and production leave them unset)
+    if os.environ.get("DLMS_ATTN_VARIANT"):
+        L.dlms_attention_variant(int(os.environ["DLMS_ATTN_VARIANT"]))
+    if os.environ.get("DLMS_GEMM_TILE"):
+        L.dlms_gemm_force_tile(int(os.environ["DLMS_GEMM_TILE"]))
     L.dlms_error_string.argtypes = [ctypes.c_int]
     L.dlms_error_string.restype = ctypes.c_char_p
     L.dlms_gemm_epi_size.restype = ctypes.c_int
