@@ -252,6 +252,15 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         out = argmax_out
     else:
         raise ValueError(f"unknown epilogue {epi}")
+    # the LDS-staged epilogue stores 16 B per lane: rows and bases must be 16-B aligned
+    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_PARTIAL, EPI_QKV):
+        t = q_out if epi == EPI_QKV else out
+        per = 4 if epi == EPI_PARTIAL else 8
+        ld = t.stride(1) if epi == EPI_PARTIAL else t.stride(0)
+        if t.data_ptr() % 16 or ld % per or (epi == EPI_PARTIAL and t.stride(0) % per):
+            raise ValueError("gemm: output rows must be 16-byte aligned")
+        if epi == EPI_QKV and (k_cache.data_ptr() % 16 or v_cache.data_ptr() % 16):
+            raise ValueError("gemm: KV cache must be 16-byte aligned")
     if fp8:
         if epi in (EPI_GELU_ERF, EPI_F32):
             raise ValueError("fp8 GEMM: epilogue not instantiated")

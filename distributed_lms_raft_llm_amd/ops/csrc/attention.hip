@@ -203,7 +203,11 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
     }
 }
 
-static int g_attn_variant = 0;  // tuning override: 0 = (unroll 4), 1 = (8), 2 = (4, nt), 3 = (8, nt)
+// Default: 4-deep unroll with non-temporal K/V loads (the cache is streamed once per layer; keeping
+// it out of L2/MALL leaves them to the weights): +6 % whole-step at 1024 queries, +4.5 % at 256
+// (profiles/r1_attention_variants.log, in-situ A/B in profiles/r1_bench_lines.jsonl).
+// Tuning override: 0 = (unroll 4, nt), 1 = (8), 2 = (4, plain), 3 = (8, nt).
+static int g_attn_variant = 0;
 extern "C" void dlms_attention_variant(int v) { g_attn_variant = v; }
 
 extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
@@ -218,9 +222,9 @@ extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, con
     };
     switch (g_attn_variant) {
         case 1: launch(attn_wave_kernel<8, false>); break;
-        case 2: launch(attn_wave_kernel<4, true>); break;
+        case 2: launch(attn_wave_kernel<4, false>); break;
         case 3: launch(attn_wave_kernel<8, true>); break;
-        default: launch(attn_wave_kernel<4, false>); break;
+        default: launch(attn_wave_kernel<4, true>); break;
     }
     return hipGetLastError();
 }

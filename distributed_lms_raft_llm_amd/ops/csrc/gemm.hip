@@ -270,6 +270,64 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
         return;
     }
 
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_PARTIAL ||
+                  EPI == EPI_QKV) {
+        // LDS-staged store: the MFMA layout puts 16 consecutive columns on 16 lanes (2-4 B each), so
+        // direct stores write 32-64 B pieces; staging the tile through LDS (padded rows: the four
+        // lane groups' rows land 64 B apart, conflict-free) turns the write-out into full 16-B-per-lane
+        // row stores.  The QKV scatter moves whole 8-column chunks (a chunk never straddles a head).
+        constexpr int OB = EPI == EPI_PARTIAL ? 4 : 2;
+        constexpr int SROW = BN * OB + 16;
+        constexpr int CPR = BN * OB / 16;  // 16-B chunks per tile row
+        __syncthreads();                   // every wave is done reading the last ring stage
+        const int lrow0 = wm * WTM + (lane >> 4) * 4;
+        const int lcol0 = wn * WTN + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const float bv = (EPI != EPI_PARTIAL && ep.bias) ? ep.bias[n0 + lcol0 + j * 16] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc[i][j][r] + bv;
+                    if constexpr (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+                    if constexpr (EPI == EPI_GELU_ERF) v = gelu_erf(v);
+                    char* dst = smem + (lrow0 + i * 16 + r) * SROW + (lcol0 + j * 16) * OB;
+                    if constexpr (OB == 4)
+                        *reinterpret_cast<float*>(dst) = v;
+                    else
+                        *reinterpret_cast<bf16_t*>(dst) = f32_to_bf16(v);
+                }
+        }
+        __syncthreads();
+        for (int c = tid; c < BM * CPR; c += NT) {
+            const int lr = c / CPR, ch = c - lr * CPR;
+            const int row = m0 + lr;
+            if (row >= M) continue;
+            const uint4 val = *reinterpret_cast<const uint4*>(smem + lr * SROW + ch * 16);
+            const int col = n0 + ch * (16 / OB);
+            if constexpr (EPI == EPI_PARTIAL) {
+                *reinterpret_cast<uint4*>(reinterpret_cast<float*>(ep.out) + (size_t)split * ep.split_stride +
+                                          (size_t)row * ep.ldo + col) = val;
+            } else if constexpr (EPI == EPI_QKV) {
+                const int part = col / ep.d_local;
+                const int within = col - part * ep.d_local;
+                bf16_t* dst;
+                if (part == 0) {
+                    dst = ep.q_out + (size_t)row * ep.ldq + within;
+                } else {
+                    const int head = within >> 6, dim = within & 63;
+                    dst = (part == 1 ? ep.k_cache : ep.v_cache) +
+                          (((size_t)ep.row_slot[row] * ep.n_heads + head) * ep.t_max + ep.row_pos[row]) * 64 + dim;
+                }
+                *reinterpret_cast<uint4*>(dst) = val;
+            } else {
+                *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(ep.out) + (size_t)row * ep.ldo + col) = val;
+            }
+        }
+        return;
+    }
+
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int col = col_base + j * 16;
@@ -315,7 +373,9 @@ template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN>
 static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
     const int tiles = ((M + BM - 1) / BM) * (N / BN) * (EPI == EPI_PARTIAL ? ep.split_k : 1);
-    const size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
+    size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
+    const size_t stage_out = (size_t)BM * (BN * (EPI == EPI_PARTIAL ? 4 : 2) + 16);  // LDS-staged epilogue
+    if (EPI != EPI_ARGMAX && EPI != EPI_F32 && stage_out > lds) lds = stage_out;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN>),
