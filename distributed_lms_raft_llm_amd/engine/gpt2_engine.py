@@ -23,6 +23,7 @@ No host round trip happens inside a step; the host only checks the stop flags ev
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 
@@ -74,6 +75,26 @@ def passthrough(prompts, T: int, eos: int):
     return out, run, norm
 
 
+@dataclass
+class _Rows:
+    """Activation buffers of one contiguous range of batch rows (the whole batch, or one half of it
+    in the overlapped decode step) plus the residual update still pending for the next LayerNorm."""
+    x: torch.Tensor
+    parts: torch.Tensor
+    h: torch.Tensor
+    q: torch.Tensor
+    att: torch.Tensor
+    ff: torch.Tensor
+    row_slot: torch.Tensor
+    row_pos: torch.Tensor
+    row_kvlen: torch.Tensor
+    M: int
+    h8: torch.Tensor | None = None
+    hsc: torch.Tensor | None = None
+    ln_out: dict | None = None
+    pend: tuple = (None, 0, None)
+
+
 def _bucket(n: int) -> int:
     for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024):
         if n <= b:
@@ -84,9 +105,14 @@ def _bucket(n: int) -> int:
 class HipGPT2Engine:
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
-                 check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16"):
+                 check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16",
+                 overlap: bool | None = None, overlap_min_batch: int = 512):
         """``weight_dtype="fp8"``: W8A8 OCP-e4m3 MFMA GEMMs for QKV, c_fc and the LM head (activation
-        rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path."""
+        rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path.
+        ``overlap``: decode batches of >= ``overlap_min_batch`` rows run as two staggered
+        half-batches on two streams (attention of one beside the GEMMs of the other); default from
+        ``DLMS_OVERLAP`` (off unless it is "1": measured 0.79x at 1024 queries, where two M=512
+        GEMM phases cost more than the attention they hide -- profiles/r1_overlap_ab.jsonl)."""
         if not torch.cuda.is_available():
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
@@ -119,6 +145,11 @@ class HipGPT2Engine:
         self.max_length = max_length
         self.use_graph = use_graph
         self.check_every = check_every
+        if overlap is None:
+            overlap = os.environ.get("DLMS_OVERLAP", "0") == "1"
+        self.overlap = bool(overlap)
+        self.overlap_min_batch = max(2, int(overlap_min_batch))
+        self._side_stream: torch.cuda.Stream | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._alloc_state()
 
@@ -214,67 +245,147 @@ class HipGPT2Engine:
         ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=s)
         return parts, s, bias
 
+    def _rows(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
+              h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None) -> "_Rows":
+        """Bundle the activation buffers of one row range for the per-layer phase functions."""
+        fp8 = self.w.fp8
+        r = _Rows(x=x[:M], parts=parts, h=h[:M], q=q[:M], att=att[:M], ff=ff[:M], row_slot=row_slot,
+                  row_pos=row_pos, row_kvlen=row_kvlen, M=M, h8=h8[:M] if fp8 else None,
+                  hsc=hsc[:M] if fp8 else None)
+        r.ln_out = (dict(out_bf16=None, want_out=False, out_fp8=r.h8, out_fp8_scale=r.hsc) if fp8
+                    else dict(out_bf16=r.h))
+        return r
+
+    def _attn_in(self, r: "_Rows", li: int):
+        """LN1 (folding the pending residual update) -> QKV GEMM (+ K/V scattered into the cache)."""
+        lw, eps, pend = self.w.layers[li], self.cfg.layer_norm_epsilon, r.pend
+        kc, vc = self.kv[li, 0], self.kv[li, 1]
+        ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
+        if self.w.fp8:
+            ops.gemm(r.h8, lw.w_qkv8, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
+                     row_slot=r.row_slot, row_pos=r.row_pos, a_scale=r.hsc, w_scale=lw.s_qkv)
+        else:
+            ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
+                     row_slot=r.row_slot, row_pos=r.row_pos)
+
+    def _attn(self, r: "_Rows", li: int):
+        ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att)
+
+    def _attn_out_mlp(self, r: "_Rows", li: int):
+        """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
+        lw, eps = self.w.layers[li], self.cfg.layer_norm_epsilon
+        pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M)
+        ops.add_layernorm(r.x, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
+        if self.w.fp8:
+            ops.gemm(r.h8, lw.w_fc8, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff, a_scale=r.hsc, w_scale=lw.s_fc)
+        else:
+            ops.gemm(r.h, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff)
+        r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M)
+
+    def _final_ln(self, r: "_Rows", final_h: torch.Tensor | None):
+        w, eps, pend = self.w, self.cfg.layer_norm_epsilon, r.pend
+        if w.fp8:
+            fin = r.ln_out if final_h is not None else dict(want_out=False)
+            ops.add_layernorm(r.x, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **fin)
+        else:
+            ops.add_layernorm(r.x, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2],
+                              out_bf16=final_h, want_out=final_h is not None)
+
     def _layers(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
                 final_h: torch.Tensor | None, h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None):
         """All blocks on rows [0, M) of the residual ``x`` (updated in place), then ln_f into
         ``final_h`` (or only the last residual update when ``final_h`` is None).  fp8 weights: the
         LayerNorms emit row-scaled e4m3 into ``h8``/``hsc`` for the W8A8 QKV / c_fc GEMMs, and the
         ln_f output goes there too (``final_h`` then only says whether it is wanted)."""
-        w, cfg = self.w, self.cfg
-        eps = cfg.layer_norm_epsilon
-        xs, hs, qs, ats, ffs = x[:M], h[:M], q[:M], att[:M], ff[:M]
-        fp8 = w.fp8
-        ln_out = dict(out_bf16=None, want_out=False, out_fp8=h8[:M] if fp8 else None,
-                      out_fp8_scale=hsc[:M] if fp8 else None) if fp8 else dict(out_bf16=hs)
-        pend = (None, 0, None)
-        for li, lw in enumerate(w.layers):
-            kc, vc = self.kv[li, 0], self.kv[li, 1]
-            ops.add_layernorm(xs, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **ln_out)
-            if fp8:
-                ops.gemm(h8[:M], lw.w_qkv8, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
-                         row_slot=row_slot, row_pos=row_pos, a_scale=hsc[:M], w_scale=lw.s_qkv)
-            else:
-                ops.gemm(hs, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=qs, k_cache=kc, v_cache=vc,
-                         row_slot=row_slot, row_pos=row_pos)
-            ops.row_attention(qs, kc, vc, row_slot, row_kvlen, out=ats)
-            pend = self._row_parallel(ats, lw.w_o, lw.b_o, parts, M)
-            ops.add_layernorm(xs, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **ln_out)
-            if fp8:
-                ops.gemm(h8[:M], lw.w_fc8, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs, a_scale=hsc[:M], w_scale=lw.s_fc)
-            else:
-                ops.gemm(hs, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=ffs)
-            pend = self._row_parallel(ffs, lw.w_p, lw.b_p, parts, M)
-        if fp8:
-            fin = ln_out if final_h is not None else dict(want_out=False)
-            ops.add_layernorm(xs, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **fin)
-        else:
-            ops.add_layernorm(xs, w.lnf_g, w.lnf_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2],
-                              out_bf16=final_h, want_out=final_h is not None)
+        r = self._rows(x, parts, h, q, att, ff, row_slot, row_pos, row_kvlen, M, h8, hsc)
+        for li in range(len(self.w.layers)):
+            self._attn_in(r, li)
+            self._attn(r, li)
+            self._attn_out_mlp(r, li)
+        self._final_ln(r, final_h)
 
     def _lm_head_and_update(self, hidden: torch.Tensor, B: int, penalty: float, seen: torch.Tensor | None = None,
-                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None):
+                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0):
         """LM head with the fused penalty + argmax on ``hidden`` (bf16, or e4m3 with ``hscale``),
-        then the greedy bookkeeping.  Rows map to slots [0, B) or through ``slot_map``."""
+        then the greedy bookkeeping.  Rows map to slots [lo, lo + B) or through ``slot_map``."""
         cfg = self.cfg
-        seen_rows = self.seen[:B] if seen is None else seen
+        hi = lo + B
+        seen_rows = self.seen[lo:hi] if seen is None else seen
         if hidden.dtype == ops.FP8:
-            ops.gemm(hidden, self.w.lm_head8, ops.EPI_ARGMAX, argmax_out=self.key_parts[:B], seen=seen_rows,
+            ops.gemm(hidden, self.w.lm_head8, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                      vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty, a_scale=hscale,
                      w_scale=self.w.s_lm)
         else:
-            ops.gemm(hidden, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[:B], seen=seen_rows,
+            ops.gemm(hidden, self.w.lm_head, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                      vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
-        keys = self._gather_keys(B)
+        if lo:
+            if self.tp_size > 1:
+                raise ValueError("row-offset LM head is TP=1 only")
+            keys = self.key_parts[lo:hi]
+        else:
+            keys = self._gather_keys(B)
         if slot_map is None:
-            ops.decode_update(keys, self.lens[:B], self.finished[:B], self.out_tokens[:B],
-                              self.seen[:B], self.cur_tok[:B], self.cur_pos[:B], self.cur_kvlen[:B], self.w.wte,
-                              self.w.wpe, self.x[:B], cfg.eos_token_id, self.max_length)
+            ops.decode_update(keys, self.lens[lo:hi], self.finished[lo:hi], self.out_tokens[lo:hi],
+                              self.seen[lo:hi], self.cur_tok[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi],
+                              self.w.wte, self.w.wpe, self.x[lo:hi], cfg.eos_token_id, self.max_length)
         else:
             ops.decode_update(keys, self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
                               self.cur_kvlen, self.w.wte, self.w.wpe, self.x, cfg.eos_token_id, self.max_length,
                               slot_map=slot_map)
 
+    def _overlap_ok(self, B: int) -> bool:
+        return self.overlap and self.tp_size == 1 and B >= self.overlap_min_batch and B % 2 == 0
+
+    def _decode_step_overlap(self, B: int, penalty: float):
+        """Decode step as two half-batches on two HIP streams, staggered by one phase so that one
+        half's HBM-bound KV-cache stream (attention) runs beside the other half's MFMA/L2-bound
+        GEMM phase.  Per half the step alternates phases
+            G(0) A(0) G(1) A(1) ... A(L-1) G(L)
+        with G(l) = [out-proj, LN2, c_fc, c_proj of layer l-1] + LN1 + QKV of layer l (G(L) ends in
+        ln_f + LM head + decode_update) and A(l) = attention of layer l.  GEMM phases of the two
+        halves are serialised (G_a(l) -> G_b(l) -> G_a(l+1) ...) by cross-stream events, so the
+        steady state pairs A_a(l) with G_b(l) and A_b(l) with G_a(l+1).  Captured as one hipGraph:
+        the event edges become graph dependencies and the two branches run concurrently."""
+        half = B // 2
+        cur = torch.cuda.current_stream(self.device)
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(device=self.device)
+        side = self._side_stream
+        side.wait_stream(cur)
+        fp8 = self.w.fp8
+        halves = []
+        for lo, hi in ((0, half), (half, B)):
+            r = self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
+                           self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], hi - lo,
+                           self.h8[lo:hi] if fp8 else None, self.hsc[lo:hi] if fp8 else None)
+            halves.append((lo, r))
+        streams = (cur, side)
+        L = len(self.w.layers)
+        last_gemm = None
+        for p in range(L + 1):
+            for (lo, r), s in zip(halves, streams):
+                with torch.cuda.stream(s):
+                    if last_gemm is not None:
+                        s.wait_event(last_gemm)
+                    if p > 0:
+                        self._attn_out_mlp(r, p - 1)
+                    if p < L:
+                        self._attn_in(r, p)
+                    else:
+                        self._final_ln(r, r.h)
+                        if fp8:
+                            self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
+                        else:
+                            self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
+                    last_gemm = torch.cuda.Event()
+                    last_gemm.record(s)
+                    if p < L:
+                        self._attn(r, p)
+        cur.wait_stream(side)
+
     def _decode_step(self, B: int, penalty: float):
+        if self._overlap_ok(B):
+            return self._decode_step_overlap(B, penalty)
         self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
                      self.cur_kvlen[:B], B, final_h=self.h[:B], h8=self.h8, hsc=self.hsc)
         if self.w.fp8:

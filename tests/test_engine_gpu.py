@@ -77,6 +77,21 @@ def test_graph_replay_equals_eager():
     assert a == b
 
 
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_overlapped_half_batch_step_equals_serial(use_graph):
+    """The two-stream staggered decode step (attention of one half-batch beside the GEMMs of the
+    other) computes exactly what the single-stream step computes."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [32] * 6 + [9, 17, 3, 25], seed=5)
+    ov = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=True, overlap_min_batch=2)
+    assert ov._overlap_ok(16)
+    a = ov.generate(prompts)
+    b = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=False).generate(prompts)
+    assert a == b
+
+
 def test_continuous_batching_matches_static():
     """Requests admitted into free slots of a running batch (8 slots, 14 staggered requests)
     produce what a static batch of each request alone produces."""
