@@ -150,6 +150,7 @@ class HipGPT2Engine:
         self.overlap = bool(overlap)
         self.overlap_min_batch = max(2, int(overlap_min_batch))
         self._side_stream: torch.cuda.Stream | None = None
+        self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._alloc_state()
 
@@ -412,6 +413,12 @@ class HipGPT2Engine:
             self._graphs[key] = g
         return g
 
+    def _stop_flags(self) -> torch.Tensor:
+        """Two pinned int32 host words for the lagged all-finished check in ``generate``."""
+        if self._flags is None:
+            self._flags = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        return self._flags
+
     def _snapshot_state(self, B: int):
         return [t[:B].clone() for t in (self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok,
                                         self.cur_pos, self.cur_kvlen, self.x)]
@@ -449,27 +456,29 @@ class HipGPT2Engine:
         if min(lens) < 1 or max(lens) > T:
             raise ValueError("prefill: prompt lengths must be in [1, max_length]")
         R = sum(lens)
-        tokens = torch.tensor([t for p in prompts for t in p], dtype=torch.int32)
-        pos = torch.tensor([i for L in lens for i in range(L)], dtype=torch.int32)
-        slot = torch.tensor([slots[b] for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32)
-        last = torch.tensor(np.cumsum(lens) - 1, dtype=torch.int32)
-
-        # host-built per-sequence state, scattered into the chosen slots
-        out_tok = torch.zeros(n, T, dtype=torch.int32)
-        seen = torch.zeros(n, self.seen_words, dtype=torch.int32)
-        for b, p in enumerate(prompts):
-            out_tok[b, : len(p)] = torch.tensor(p, dtype=torch.int32)
-            seen[b] = torch.from_numpy(seen_bitmap(p, self.seen_words))
-        lens_t = torch.tensor(lens, dtype=torch.int32)
-        fin = (lens_t >= T).to(torch.int32)
-        tokens_d, pos_d, slot_d, last_d, slots_d, out_d, seen_d, lens_d, fin_d = (
-            t.to(dev, non_blocking=True)
-            for t in (tokens, pos, slot, last, torch.tensor(slots, dtype=torch.int32), out_tok, seen, lens_t, fin))
+        # packed token / position / slot arrays built with numpy (no per-prompt Python loops: a
+        # 1024-prompt admission used to spend ~20 ms of host time here with the GPU idle)
+        lens_np = np.asarray(lens, dtype=np.int64)
+        ends = np.cumsum(lens_np)
+        tok_np = np.fromiter((t for p in prompts for t in p), dtype=np.int64, count=R)
+        if tok_np.min() < 0 or tok_np.max() >= cfg.vocab_size:
+            raise ValueError("prefill: token id out of range")
+        pos_np = np.arange(R, dtype=np.int64) - np.repeat(ends - lens_np, lens_np)
+        slot_np = np.repeat(np.asarray(slots, dtype=np.int64), lens_np)
+        tokens_d, pos_d, slot_d, last_d, slots_d, lens_d = (
+            torch.from_numpy(a.astype(np.int32)).to(dev, non_blocking=True)
+            for a in (tok_np, pos_np, slot_np, ends - 1, np.asarray(slots), lens_np))
+        fin_d = (lens_d >= T).to(torch.int32)
+        # per-sequence state scattered into the chosen slots on the device
         idx = slots_d.long()
-        self.out_tokens.index_copy_(0, idx, out_d)
-        self.seen.index_copy_(0, idx, seen_d)
+        self.out_tokens.index_fill_(0, idx, 0)
+        self.out_tokens.index_put_((slot_d.long(), pos_d.long()), tokens_d)
+        self.seen.index_fill_(0, idx, 0)
+        ops.seen_set(self.seen, slot_d, tokens_d)
         self.lens.index_copy_(0, idx, lens_d)
         self.finished.index_copy_(0, idx, fin_d)
+        # the LM head of the first token reads the prompts' bitmaps as rows [0, n)
+        seen_d = self.seen.index_select(0, idx)
 
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         f32, bf = torch.float32, torch.bfloat16
@@ -549,8 +558,8 @@ class HipGPT2Engine:
             return []
         idx = torch.tensor(slots, dtype=torch.long, device=self.device)
         lens = self.lens.index_select(0, idx).cpu().tolist()
-        toks = self.out_tokens.index_select(0, idx).cpu()
-        return [toks[i, : lens[i]].tolist() for i in range(len(slots))]
+        toks = self.out_tokens.index_select(0, idx).cpu().tolist()
+        return [toks[i][: lens[i]] for i in range(len(slots))]
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
@@ -584,6 +593,11 @@ class HipGPT2Engine:
         steps_max = T - min(len(p) for p in prompts) - 1
         graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
         steps = 0
+        # Stop check one chunk behind: the all-finished flag of chunk k is copied to pinned host
+        # memory asynchronously and read after chunk k+1 has been enqueued, so the GPU never idles
+        # on the host round trip (at most one extra chunk of no-op steps once every row is done).
+        flags = self._stop_flags()
+        pending = None
         while steps < steps_max:
             chunk = min(self.check_every, steps_max - steps)
             for _ in range(chunk):
@@ -592,12 +606,21 @@ class HipGPT2Engine:
                 else:
                     self._decode_step(B, repetition_penalty)
             steps += chunk
-            if steps < steps_max and bool(self.finished[:n].all()):
+            if steps >= steps_max:
                 break
+            slot = (steps // self.check_every) & 1
+            flags[slot].copy_(self.finished[:n].min(), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            if pending is not None:
+                pending[0].synchronize()
+                if int(flags[pending[1]]):
+                    break
+            pending = (ev, slot)
         ev2.record()
         lens = self.lens[:n].cpu().tolist()
-        toks = self.out_tokens[:n].cpu()
-        res = [toks[b, : lens[b]].tolist() for b in range(n)]
+        toks = self.out_tokens[:n].cpu().tolist()  # one conversion, not one per row
+        res = [toks[b][: lens[b]] for b in range(n)]
         if stats is not None:
             ev2.synchronize()
             stats.batch += n

@@ -98,6 +98,7 @@ def _bind(L):
         "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I,
                                I, I, I, P],
         "dlms_argmax_reduce": [P, I, ctypes.c_longlong, P, I, P],
+        "dlms_seen_set": [P, P, I, P, I, P],
         "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
         "dlms_mean_pool": [P, P, P, P, I, I, P],
         "dlms_cosine": [P, P, P, I, I, I, F, P],
@@ -429,6 +430,22 @@ def argmax_reduce(parts: torch.Tensor, out: torch.Tensor | None = None) -> torch
         raise ValueError("argmax_reduce: out too short")
     _check(lib().dlms_argmax_reduce(_p(parts), P, parts.stride(0), _p(out), B, _stream()), "dlms_argmax_reduce")
     return out
+
+
+def seen_set(seen: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor):
+    """OR the bit of every ``tokens[i]`` into ``seen[rows[i]]`` (int32 bitmap rows of V/32 words).
+    Callers validate rows (< seen.shape[0]) and ids on the host before upload; the kernel also skips
+    ids outside [0, 32 * words)."""
+    _req(seen, torch.int32, "seen", 2)
+    _req(rows, torch.int32, "rows", 1)
+    _req(tokens, torch.int32, "tokens", 1)
+    R = tokens.numel()
+    if rows.numel() != R or not seen.is_contiguous():
+        raise ValueError("seen_set: one row per token, contiguous bitmap")
+    if R == 0:
+        return seen
+    _check(lib().dlms_seen_set(_p(tokens), _p(rows), R, _p(seen), seen.shape[1], _stream()), "dlms_seen_set")
+    return seen
 
 
 def decode_update(keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok, cur_pos, cur_kvlen, wte, wpe, x,

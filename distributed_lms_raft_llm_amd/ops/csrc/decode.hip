@@ -135,3 +135,22 @@ extern "C" hipError_t dlms_argmax_reduce(const unsigned long long* keys, int npa
     hipLaunchKernelGGL(argmax_reduce_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, out, B);
     return hipGetLastError();
 }
+
+// Prefill bookkeeping on the device: set the repetition-penalty bit of every prompt token in its
+// sequence's seen bitmap (rows pre-zeroed by the caller).  One thread per packed prompt token;
+// duplicate tokens of a row OR the same bit, so the result does not depend on the order.
+__global__ __launch_bounds__(256) void seen_set_kernel(const int* __restrict__ tokens, const int* __restrict__ rows,
+                                                       int R, unsigned int* seen, int seen_words) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= R) return;
+    const int t = tokens[i];
+    if (t < 0 || (t >> 5) >= seen_words) return;  // the host validates ids; never write out of the row
+    atomicOr(seen + (size_t)rows[i] * seen_words + (t >> 5), 1u << (t & 31));
+}
+
+extern "C" hipError_t dlms_seen_set(const int* tokens, const int* rows, int R, unsigned int* seen, int seen_words,
+                                    hipStream_t stream) {
+    if (R <= 0 || seen_words <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(seen_set_kernel, dim3((R + 255) / 256), dim3(256), 0, stream, tokens, rows, R, seen, seen_words);
+    return hipGetLastError();
+}
