@@ -67,10 +67,11 @@ class HipBertEncoder:
         kc = torch.empty(n, nh, S, 64, dtype=bf, device=dev)
         vc = torch.empty_like(kc)
         parts = torch.empty(1, R, H, dtype=torch.float32, device=dev)
+        tiles = ops.AttnTiles(lens, dev)  # bidirectional: every row of a sequence sees all its keys
         for lw in self.layers:
             ops.gemm(h, lw["w_qkv"], ops.EPI_QKV, bias=lw["b_qkv"], q_out=q, k_cache=kc, v_cache=vc, row_slot=seq,
                      row_pos=pos)
-            ops.row_attention(q, kc, vc, seq, kvlen, out=att)
+            ops.tile_attention(q, kc, vc, seq, kvlen, tiles, out=att)
             ops.gemm(att, lw["w_o"], ops.EPI_PARTIAL, out=parts, split_k=1)
             ops.add_layernorm(x, lw["ln1_g"], lw["ln1_b"], eps, parts=parts, nsplit=1, bias=lw["b_o"], out_bf16=h,
                               store_normed=True)

@@ -93,6 +93,7 @@ class _Rows:
     hsc: torch.Tensor | None = None
     ln_out: dict | None = None
     pend: tuple = (None, 0, None)
+    tiles: "ops.AttnTiles | None" = None  # packed prompts: MFMA tile attention instead of per-row
 
 
 def _bucket(n: int) -> int:
@@ -247,12 +248,13 @@ class HipGPT2Engine:
         return parts, s, bias
 
     def _rows(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
-              h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None) -> "_Rows":
+              h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None,
+              tiles: "ops.AttnTiles | None" = None) -> "_Rows":
         """Bundle the activation buffers of one row range for the per-layer phase functions."""
         fp8 = self.w.fp8
         r = _Rows(x=x[:M], parts=parts, h=h[:M], q=q[:M], att=att[:M], ff=ff[:M], row_slot=row_slot,
                   row_pos=row_pos, row_kvlen=row_kvlen, M=M, h8=h8[:M] if fp8 else None,
-                  hsc=hsc[:M] if fp8 else None)
+                  hsc=hsc[:M] if fp8 else None, tiles=tiles)
         r.ln_out = (dict(out_bf16=None, want_out=False, out_fp8=r.h8, out_fp8_scale=r.hsc) if fp8
                     else dict(out_bf16=r.h))
         return r
@@ -270,7 +272,10 @@ class HipGPT2Engine:
                      row_slot=r.row_slot, row_pos=r.row_pos)
 
     def _attn(self, r: "_Rows", li: int):
-        ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att)
+        if r.tiles is not None:  # packed prompts (K6): 16-query MFMA tiles
+            ops.tile_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, r.tiles, out=r.att)
+        else:  # decode (K5): one query per sequence, a pure KV stream
+            ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att)
 
     def _attn_out_mlp(self, r: "_Rows", li: int):
         """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
@@ -293,12 +298,13 @@ class HipGPT2Engine:
                               out_bf16=final_h, want_out=final_h is not None)
 
     def _layers(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
-                final_h: torch.Tensor | None, h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None):
+                final_h: torch.Tensor | None, h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None,
+                tiles: "ops.AttnTiles | None" = None):
         """All blocks on rows [0, M) of the residual ``x`` (updated in place), then ln_f into
         ``final_h`` (or only the last residual update when ``final_h`` is None).  fp8 weights: the
         LayerNorms emit row-scaled e4m3 into ``h8``/``hsc`` for the W8A8 QKV / c_fc GEMMs, and the
         ln_f output goes there too (``final_h`` then only says whether it is wanted)."""
-        r = self._rows(x, parts, h, q, att, ff, row_slot, row_pos, row_kvlen, M, h8, hsc)
+        r = self._rows(x, parts, h, q, att, ff, row_slot, row_pos, row_kvlen, M, h8, hsc, tiles)
         for li in range(len(self.w.layers)):
             self._attn_in(r, li)
             self._attn(r, li)
@@ -493,7 +499,8 @@ class HipGPT2Engine:
         if self.w.fp8:
             h8 = torch.zeros(R, self.w.k_fp8, dtype=ops.FP8, device=dev)  # K padding stays zero
             hsc = torch.empty(R, dtype=f32, device=dev)
-        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None, h8=h8, hsc=hsc)
+        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None, h8=h8, hsc=hsc,
+                     tiles=ops.AttnTiles(lens, dev))
         hl = ops.layernorm_gather(x, last_d, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon)
         hsc_l = None
         if self.w.fp8:
@@ -528,7 +535,8 @@ class HipGPT2Engine:
         if self.w.fp8:
             h8 = torch.zeros(R, self.w.k_fp8, dtype=ops.FP8, device=dev)
             hsc = torch.empty(R, device=dev)
-        self._layers(x, parts, h, q, att, ff, slot, pos, pos + 1, R, final_h=None, h8=h8, hsc=hsc)
+        self._layers(x, parts, h, q, att, ff, slot, pos, pos + 1, R, final_h=None, h8=h8, hsc=hsc,
+                     tiles=ops.AttnTiles(lens, dev))
         return ops.layernorm_gather(x, last, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon).float()
 
     # ------------------------------------------------------------------ slot API (continuous batching)

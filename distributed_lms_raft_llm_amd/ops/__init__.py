@@ -94,6 +94,7 @@ def _bind(L):
         "dlms_quantize_rows_fp8": [P, I, P, I, P, I, I, P],
         "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
         "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
+        "dlms_tile_attention": [P, I, P, P, P, P, P, I, P, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, P],
         "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I,
                                I, I, I, P],
@@ -402,6 +403,58 @@ def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     fn = lib().dlms_attention if impl == "wave" else lib().dlms_row_attention
     _check(fn(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen), _p(out), out.stride(0), R, H,
               T, float(sc), _stream()), "attention")
+    return out
+
+
+class AttnTiles:
+    """16-query tiles of packed sequences for ``tile_attention``: int32 [ntiles, 2] (row0, nq) on
+    the device, plus the host-known number of packed rows they cover (checked against ``q``)."""
+
+    def __init__(self, lens, device):
+        import numpy as np
+
+        lens = np.asarray(list(lens), dtype=np.int64)
+        if lens.size == 0 or lens.min() < 1:
+            raise ValueError("AttnTiles: every sequence needs >= 1 row")
+        nt = (lens + 15) // 16
+        starts = np.cumsum(lens) - lens
+        seq = np.repeat(np.arange(lens.size), nt)
+        k = np.arange(int(nt.sum())) - np.repeat(np.cumsum(nt) - nt, nt)
+        row0 = starts[seq] + 16 * k
+        nq = np.minimum(16, lens[seq] - 16 * k)
+        self.rows = int(lens.sum())
+        self.n = int(nt.sum())
+        self.t = torch.from_numpy(np.stack([row0, nq], axis=1).astype(np.int32)).to(device, non_blocking=True)
+
+
+def tile_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
+                   row_kvlen: torch.Tensor, tiles: AttnTiles, out: torch.Tensor | None = None,
+                   scale: float | None = None):
+    """MFMA attention over 16-query tiles (prefill / encoder): same contract as ``row_attention``
+    (row r attends keys [0, row_kvlen[r]) of slot row_slot[r]); every tile's rows belong to one
+    sequence (``AttnTiles`` builds them from the packed sequence lengths)."""
+    _req(q, torch.bfloat16, "q", 2)
+    _req(k_cache, torch.bfloat16, "k_cache", 4)
+    _req(v_cache, torch.bfloat16, "v_cache", 4)
+    _req(row_slot, torch.int32, "row_slot", 1)
+    _req(row_kvlen, torch.int32, "row_kvlen", 1)
+    R = q.shape[0]
+    S, H, T, hd = k_cache.shape
+    if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64:
+        raise ValueError("tile_attention: bad shapes")
+    if not k_cache.is_contiguous() or not v_cache.is_contiguous():
+        raise ValueError("tile_attention: caches must be contiguous")
+    if tiles.rows > R or row_slot.numel() < tiles.rows or row_kvlen.numel() < tiles.rows:
+        raise ValueError("tile_attention: tiles cover more rows than q / index arrays hold")
+    if out is None:
+        out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=q.device)
+    _req(out, torch.bfloat16, "out", 2)
+    if out.shape[0] < tiles.rows or q.stride(0) % 8 or out.stride(0) % 8 or q.data_ptr() % 16 or out.data_ptr() % 16:
+        raise ValueError("tile_attention: rows must be 16-byte aligned")
+    sc = (1.0 / 8.0) if scale is None else scale
+    _check(lib().dlms_tile_attention(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
+                                     _p(tiles.t), tiles.n, _p(out), out.stride(0), H, T, float(sc), _stream()),
+           "tile_attention")
     return out
 
 

@@ -238,3 +238,170 @@ extern "C" hipError_t dlms_row_attention(const void* q, int ldq, const void* kc,
                        reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// MFMA tile attention (K6 prefill, K14 BERT encoder): ONE WAVE per (16-query tile, head), four
+// heads per workgroup.  A tile is up to 16 consecutive packed rows of ONE sequence (host-built
+// tile list: row0, nq); query row r attends keys [0, row_kvlen[r]) of slot row_slot[row0]
+// (causal prefill passes kvlen = pos + 1, the bidirectional encoder the sequence length).
+//
+// Per 32-key step (v_mfma_f32_16x16x32_bf16, 8 MFMAs):
+//   S^T[32 keys x 16 queries] = K . Q^T   -- "swapped" orientation: lane l holds the scores of
+//       query l&15 for keys 4g..4g+3 and 16+4g..16+4g+3 (g = l>>4), so the online softmax of a
+//       query is 8 in-register values + two cross-group shuffles, and the probabilities ARE the
+//       A operand of the next product (k order permuted: slot 8g+j <-> those keys);
+//   O[16 x 64] += P . V   -- V's key rows staged in LDS (4 KiB per wave, wave-private) and read
+//       back transposed with ds_read_b64_tr_b16 into B fragments whose k slots follow the same
+//       key permutation.
+// K fragments and Q come straight from global memory (16-B row chunks).  The output tile is
+// restaged through the wave's LDS so each lane stores whole 16-B row chunks.
+// EXEC stays all-ones around the transposed reads: only whole waves leave early (h >= H), every
+// loop bound is wave-uniform and out-of-range keys/queries are clamped + masked, never skipped.
+typedef short tr4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) tr4_t lds_tr4_t;
+
+__global__ __launch_bounds__(256) void attn_tile_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                        const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                                        const int* __restrict__ row_slot,
+                                                        const int* __restrict__ row_kvlen,
+                                                        const int* __restrict__ tiles, bf16_t* __restrict__ out,
+                                                        int ldo, int H, int t_max, float scale_log2) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * 4096];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int h = blockIdx.y * 4 + w;
+    if (h >= H) return;  // whole wave
+    const int row0 = tiles[2 * blockIdx.x];
+    const int nq = tiles[2 * blockIdx.x + 1];
+    const int qi = lane & 15;
+    const int g = lane >> 4;
+    const int qrow = row0 + (qi < nq ? qi : nq - 1);
+    const int slot = row_slot[row0];
+    int kvq = row_kvlen[qrow];
+    kvq = kvq < 1 ? 1 : (kvq > t_max ? t_max : kvq);
+    int kv_end = kvq;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const int other = __shfl_xor(kv_end, o, 64);
+        kv_end = other > kv_end ? other : kv_end;
+    }
+    if (qi >= nq) kvq = 0;  // padding lanes: every key masked, never stored
+
+    const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+    const bf16_t* K = kc + head_off;
+    const bf16_t* V = vc + head_off;
+    bf16x8_t qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+        qf[ks] = *reinterpret_cast<const bf16x8_t*>(q + (size_t)qrow * ldq + h * 64 + 32 * ks + 8 * g);
+
+    char* vl = smem + w * 4096;
+    float m = -INFINITY, l = 0.f;
+    f32x4_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    for (int t0 = 0; t0 < kv_end; t0 += 32) {
+        // ---- V tile -> LDS (issued first: its latency overlaps the score MFMAs) ----
+        uint4 vrow[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int key = t0 + (lane >> 3) + 8 * i;
+            key = key < kv_end ? key : kv_end - 1;
+            vrow[i] = *reinterpret_cast<const uint4*>(V + (size_t)key * 64 + (lane & 7) * 8);
+        }
+        // ---- S^T = K . Q^T (two 16-key tiles) ----
+        f32x4_t s[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            int key = t0 + 16 * tt + qi;
+            key = key < kv_end ? key : kv_end - 1;
+            const bf16x8_t k0 = *reinterpret_cast<const bf16x8_t*>(K + (size_t)key * 64 + 8 * g);
+            const bf16x8_t k1 = *reinterpret_cast<const bf16x8_t*>(K + (size_t)key * 64 + 32 + 8 * g);
+            s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[0], (f32x4_t){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[1], s[tt], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4*>(vl + ((lane >> 3) + 8 * i) * 128 + (lane & 7) * 16) = vrow[i];
+        // ---- online softmax for query qi over this lane's 8 keys ----
+        float sv[8];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int key = t0 + 16 * (j >> 2) + 4 * g + (j & 3);
+            const float v = key < kvq ? s[j >> 2][j & 3] * scale_log2 : -INFINITY;
+            sv[j] = v;
+            mx = fmaxf(mx, v);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m, mx);
+        const bool none = m_new == -INFINITY;  // no valid key yet for this query
+        const float corr = none ? 1.f : exp2f(m - m_new);
+        float psum = 0.f;
+        bf16x8_t pa;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float p = none ? 0.f : exp2f(sv[j] - m_new);
+            psum += p;
+            pa[j] = (short)f32_to_bf16(p);
+        }
+        psum += __shfl_xor(psum, 16, 64);
+        psum += __shfl_xor(psum, 32, 64);
+        l = l * corr + psum;
+        m = m_new;
+        // O rows are queries 4g + r: fetch their correction factors from lanes 4g + r
+        float cr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cr[r] = __shfl(corr, 4 * g + r, 64);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[c][r] *= cr[r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // V tile stored (wave-private region)
+        // ---- O += P . V: B fragment slot 8g+j <-> key 4g+j (j<4) / 16+4g+(j-4), column 16c + qi ----
+        const int trow = 4 * g + (qi >> 2);  // this lane supplies row (4g + q) of its group's 4x16 block
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int col = 16 * c + 4 * (qi & 3);
+            const tr4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_tr4_t*)(vl + trow * 128 + col * 2));
+            const tr4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_tr4_t*)(vl + (16 + trow) * 128 + col * 2));
+            const bf16x8_t vb = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[c], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's stores
+    }
+    // ---- normalise (queries 4g + r), restage through LDS as [16 rows][64 dims] bf16, 16-B stores ----
+    float inv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float lr = __shfl(l, 4 * g + r, 64);
+        inv[r] = lr > 0.f ? 1.f / lr : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<bf16_t*>(vl + (4 * g + r) * 128 + (16 * c + qi) * 2) = f32_to_bf16(o[c][r] * inv[r]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int chunk = lane + 64 * i;  // 16 rows x 8 chunks
+        const int r = chunk >> 3, ch = chunk & 7;
+        const uint4 val = *reinterpret_cast<const uint4*>(vl + r * 128 + ch * 16);
+        if (r < nq) *reinterpret_cast<uint4*>(out + (size_t)(row0 + r) * ldo + h * 64 + ch * 8) = val;
+    }
+}
+
+extern "C" hipError_t dlms_tile_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
+                                          const int* row_kvlen, const int* tiles, int ntiles, void* out, int ldo, int H,
+                                          int t_max, float scale, hipStream_t stream) {
+    if (ntiles <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
+    const float scale_log2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(attn_tile_kernel, dim3(ntiles, (H + 3) / 4), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
+                       reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, tiles, reinterpret_cast<bf16_t*>(out),
+                       ldo, H, t_max, scale_log2);
+    return hipGetLastError();
+}

@@ -153,6 +153,53 @@ def test_row_attention(kvlens, impl):
         torch.testing.assert_close(out[r].float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("lens", [[1, 7, 16, 17, 32, 50], [150, 3], [33]])
+def test_tile_attention_matches_fp32(lens, causal):
+    """MFMA tile attention (prefill / encoder) on packed variable-length sequences vs an fp32
+    torch softmax-attention, with 5 heads (partial last 4-head workgroup) and slots that do not
+    follow the packing order."""
+    ops = _ops()
+    H, T = 5, 160
+    R, n = sum(lens), len(lens)
+    q = _bf(R, H * 64, seed=21)
+    kc = _bf(n + 2, H, T, 64, seed=22)
+    vc = _bf(n + 2, H, T, 64, seed=23)
+    slots = [(3 * b + 1) % (n + 2) for b in range(n)]
+    assert len(set(slots)) == n
+    row_slot = torch.tensor([slots[b] for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32, device=DEV)
+    kvl = torch.tensor([(i + 1) if causal else L for L in lens for i in range(L)], dtype=torch.int32, device=DEV)
+    tiles = ops.AttnTiles(lens, DEV)
+    out = ops.tile_attention(q, kc, vc, row_slot, kvl, tiles)
+    row = 0
+    for b, L in enumerate(lens):
+        s = slots[b]
+        K, V = kc[s, :, :L].float(), vc[s, :, :L].float()          # [H, L, 64]
+        qq = q[row: row + L].float().view(L, H, 64).transpose(0, 1)  # [H, L, 64]
+        sc = torch.einsum("hqd,hkd->hqk", qq, K) / 8.0
+        if causal:
+            sc = sc.masked_fill(torch.ones(L, L, device=DEV).triu(1).bool(), float("-inf"))
+        ref = torch.einsum("hqk,hkd->hqd", torch.softmax(sc, -1), V).transpose(0, 1).reshape(L, H * 64)
+        torch.testing.assert_close(out[row: row + L].float(), ref, atol=2e-2, rtol=2e-2)
+        row += L
+
+
+def test_tile_attention_equals_row_attention_on_prefill_rows():
+    """Same inputs through both kernels (the row kernel is the decode path): outputs agree to bf16."""
+    ops = _ops()
+    H, T = 12, 64
+    lens = [32] * 9 + [5, 20]
+    R, n = sum(lens), len(lens)
+    q = _bf(R, H * 64, seed=31)
+    kc = _bf(n, H, T, 64, seed=32)
+    vc = _bf(n, H, T, 64, seed=33)
+    row_slot = torch.tensor([b for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32, device=DEV)
+    kvl = torch.tensor([i + 1 for L in lens for i in range(L)], dtype=torch.int32, device=DEV)
+    a = ops.tile_attention(q, kc, vc, row_slot, kvl, ops.AttnTiles(lens, DEV))
+    b = ops.row_attention(q, kc, vc, row_slot, kvl)
+    torch.testing.assert_close(a.float(), b.float(), atol=1.6e-2, rtol=1.6e-2)
+
+
 def test_embed_and_decode_update():
     ops = _ops()
     V, P, D, B, T = 1000, 64, 128, 3, 10
