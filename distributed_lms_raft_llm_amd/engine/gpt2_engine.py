@@ -107,13 +107,13 @@ class HipGPT2Engine:
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
                  check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16",
-                 overlap: bool | None = None, overlap_min_batch: int = 512):
+                 overlap: bool | None = None, overlap_min_batch: int = 1024, overlap_parts: int | None = None):
         """``weight_dtype="fp8"``: W8A8 OCP-e4m3 MFMA GEMMs for QKV, c_fc and the LM head (activation
         rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path.
-        ``overlap``: decode batches of >= ``overlap_min_batch`` rows run as two staggered
-        half-batches on two streams (attention of one beside the GEMMs of the other); default from
-        ``DLMS_OVERLAP`` (off unless it is "1": measured 0.79x at 1024 queries, where two M=512
-        GEMM phases cost more than the attention they hide -- profiles/r1_overlap_ab.jsonl)."""
+        ``overlap``: decode batches of >= ``overlap_min_batch`` rows run as ``overlap_parts`` row
+        ranges on as many streams (attention of one beside the GEMMs of the others); default from
+        ``DLMS_OVERLAP`` (on unless "0"; measured +1.7 % at 1024 queries, +7 % at 2048, 4 parts
+        and the serialised-halves schedule slower -- profiles/r1_overlap_ab.jsonl)."""
         if not torch.cuda.is_available():
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
@@ -147,10 +147,13 @@ class HipGPT2Engine:
         self.use_graph = use_graph
         self.check_every = check_every
         if overlap is None:
-            overlap = os.environ.get("DLMS_OVERLAP", "0") == "1"
+            overlap = os.environ.get("DLMS_OVERLAP", "1") != "0"
         self.overlap = bool(overlap)
         self.overlap_min_batch = max(2, int(overlap_min_batch))
-        self._side_stream: torch.cuda.Stream | None = None
+        self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
+        if self.overlap_parts not in (2, 3, 4):
+            raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
+        self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._alloc_state()
@@ -341,32 +344,60 @@ class HipGPT2Engine:
                               slot_map=slot_map)
 
     def _overlap_ok(self, B: int) -> bool:
-        return self.overlap and self.tp_size == 1 and B >= self.overlap_min_batch and B % 2 == 0
+        k = self.overlap_parts
+        return self.overlap and self.tp_size == 1 and B >= self.overlap_min_batch and B % k == 0
+
+    def _part_rows(self, lo: int, hi: int) -> "_Rows":
+        fp8 = self.w.fp8
+        return self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
+                          self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], hi - lo,
+                          self.h8[lo:hi] if fp8 else None, self.hsc[lo:hi] if fp8 else None)
+
+    def _part_step(self, r: "_Rows", lo: int, penalty: float):
+        """The whole decode step for one row range (rows are independent sequences)."""
+        for li in range(len(self.w.layers)):
+            self._attn_in(r, li)
+            self._attn(r, li)
+            self._attn_out_mlp(r, li)
+        self._final_ln(r, r.h)
+        if self.w.fp8:
+            self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
+        else:
+            self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
 
     def _decode_step_overlap(self, B: int, penalty: float):
-        """Decode step as two half-batches on two HIP streams, staggered by one phase so that one
-        half's HBM-bound KV-cache stream (attention) runs beside the other half's MFMA/L2-bound
-        GEMM phase.  Per half the step alternates phases
-            G(0) A(0) G(1) A(1) ... A(L-1) G(L)
-        with G(l) = [out-proj, LN2, c_fc, c_proj of layer l-1] + LN1 + QKV of layer l (G(L) ends in
-        ln_f + LM head + decode_update) and A(l) = attention of layer l.  GEMM phases of the two
-        halves are serialised (G_a(l) -> G_b(l) -> G_a(l+1) ...) by cross-stream events, so the
-        steady state pairs A_a(l) with G_b(l) and A_b(l) with G_a(l+1).  Captured as one hipGraph:
-        the event edges become graph dependencies and the two branches run concurrently."""
-        half = B // 2
+        """Decode step as ``overlap_parts`` row ranges on as many HIP streams (one hardware queue
+        each), free-running: the decode GEMMs are latency-bound (a near-constant ~12 us per launch
+        whatever M, profiles/r1_gemm_lab) and attention is HBM-bound, so independent row ranges
+        fill each other's bubbles -- the GEMMs of one part run beside the KV stream and the GEMMs
+        of the others.  Captured as one hipGraph with ``overlap_parts`` independent branches (fork
+        at the start, join at the end).
+
+        ``DLMS_OVERLAP_SERIAL=1`` (two parts only): GEMM phases of the halves serialised by
+        cross-stream events so attention of one half always pairs with the GEMMs of the other
+        (measured slower: the halves' GEMMs then cannot overlap each other)."""
+        k = self.overlap_parts
         cur = torch.cuda.current_stream(self.device)
-        if self._side_stream is None:
-            self._side_stream = torch.cuda.Stream(device=self.device)
-        side = self._side_stream
-        side.wait_stream(cur)
-        fp8 = self.w.fp8
-        halves = []
-        for lo, hi in ((0, half), (half, B)):
-            r = self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
-                           self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], hi - lo,
-                           self.h8[lo:hi] if fp8 else None, self.hsc[lo:hi] if fp8 else None)
-            halves.append((lo, r))
-        streams = (cur, side)
+        while len(self._side_streams) < k - 1:
+            self._side_streams.append(torch.cuda.Stream(device=self.device))
+        streams = [cur] + self._side_streams[: k - 1]
+        for s in streams[1:]:
+            s.wait_stream(cur)
+        step = B // k
+        parts = [(i * step, self._part_rows(i * step, (i + 1) * step)) for i in range(k)]
+        if k == 2 and os.environ.get("DLMS_OVERLAP_SERIAL", "0") == "1":
+            self._two_halves_serialised(parts, streams, penalty)
+        else:
+            for (lo, r), s in zip(parts, streams):
+                with torch.cuda.stream(s):
+                    self._part_step(r, lo, penalty)
+        for s in streams[1:]:
+            cur.wait_stream(s)
+
+    def _two_halves_serialised(self, halves, streams, penalty: float):
+        """Phases G(0) A(0) G(1) ... A(L-1) G(L) per half (G(l) = out-proj/LN2/c_fc/c_proj of
+        layer l-1 + LN1/QKV of layer l; G(L) ends in ln_f + LM head + update; A(l) = attention),
+        GEMM phases alternating between the halves (G_a(l) -> G_b(l) -> G_a(l+1) ...)."""
         L = len(self.w.layers)
         last_gemm = None
         for p in range(L + 1):
@@ -380,7 +411,7 @@ class HipGPT2Engine:
                         self._attn_in(r, p)
                     else:
                         self._final_ln(r, r.h)
-                        if fp8:
+                        if self.w.fp8:
                             self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
                         else:
                             self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
@@ -388,7 +419,6 @@ class HipGPT2Engine:
                     last_gemm.record(s)
                     if p < L:
                         self._attn(r, p)
-        cur.wait_stream(side)
 
     def _decode_step(self, B: int, penalty: float):
         if self._overlap_ok(B):

@@ -77,15 +77,18 @@ def test_graph_replay_equals_eager():
     assert a == b
 
 
-@pytest.mark.parametrize("use_graph", [True, False])
-def test_overlapped_half_batch_step_equals_serial(use_graph):
-    """The two-stream staggered decode step (attention of one half-batch beside the GEMMs of the
-    other) computes exactly what the single-stream step computes."""
+@pytest.mark.parametrize("use_graph,parts,serial", [(True, 2, False), (False, 2, False), (True, 4, False),
+                                                    (True, 2, True)])
+def test_overlapped_multi_stream_step_equals_serial(use_graph, parts, serial, monkeypatch):
+    """The multi-stream decode step (row ranges on 2-4 streams, free-running or with the
+    serialised-halves schedule) computes exactly what the single-stream step computes."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
+    monkeypatch.setenv("DLMS_OVERLAP_SERIAL", "1" if serial else "0")
     cfg, w = _setup("gpt2")
     prompts = _prompts(cfg, [32] * 6 + [9, 17, 3, 25], seed=5)
-    ov = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=True, overlap_min_batch=2)
+    ov = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=True, overlap_min_batch=2,
+                       overlap_parts=parts)
     assert ov._overlap_ok(16)
     a = ov.generate(prompts)
     b = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=False).generate(prompts)
