@@ -166,6 +166,16 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
 #pragma unroll
         for (int i = 0; i < NV4; ++i) pv[k][i] = pk[cidx[i]];
     }
+    // gamma/beta are loaded with everything else (not after the statistics: that was a second
+    // dependent memory round trip per row)
+    const float4* g4 = reinterpret_cast<const float4*>(gamma);
+    const float4* b4 = reinterpret_cast<const float4*>(beta);
+    float4 gv[NV4], bv[NV4];
+#pragma unroll
+    for (int i = 0; i < NV4; ++i) {
+        gv[i] = g4[cidx[i]];
+        bv[i] = b4[cidx[i]];
+    }
     if (bias) {
 #pragma unroll
         for (int i = 0; i < NV4; ++i) {
@@ -202,12 +212,10 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
         }
     }
     const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
-    const float4* g4 = reinterpret_cast<const float4*>(gamma);
-    const float4* b4 = reinterpret_cast<const float4*>(beta);
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < NV4; ++i) {
-        const float4 g = g4[cidx[i]], b = b4[cidx[i]];
+        const float4 g = gv[i], b = bv[i];
         if (valid[i]) {
             const float4 y = make_float4((v[i].x - mean) * rstd * g.x + b.x, (v[i].y - mean) * rstd * g.y + b.y,
                                          (v[i].z - mean) * rstd * g.z + b.z, (v[i].w - mean) * rstd * g.w + b.w);
