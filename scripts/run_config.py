@@ -18,7 +18,7 @@ rate, gate rejections, Raft failover time.  Synthetic data and random-init weigh
   2  gpt2         1 GPU, 3-node Raft + BERT gate
   3  gpt2-medium  1 GPU, continuous batching of concurrent queries, 5-node Raft
   4  gpt2-large   TP=4 over xGMI, hipGraph decode, 5-node Raft, leader killed under load
-  5  gpt2-xl      TP=8, 5-node Raft, full PDF -> gate -> LLM workflow
+  5  gpt2-xl      TP=8, fp8 (W8A8) GEMMs, 5-node Raft, full PDF -> gate -> LLM workflow
 """
 from __future__ import annotations
 
@@ -42,7 +42,8 @@ CONFIGS = {
     2: dict(model="gpt2", device="cuda", nodes=3, gate="bert", tp=1, pdf=False, kill_leader=False),
     3: dict(model="gpt2-medium", device="cuda", nodes=5, gate="bert", tp=1, pdf=False, kill_leader=False),
     4: dict(model="gpt2-large", device="cuda", nodes=5, gate="bert", tp=4, pdf=False, kill_leader=True),
-    5: dict(model="gpt2-xl", device="cuda", nodes=5, gate="bert", tp=8, pdf=True, kill_leader=False),
+    5: dict(model="gpt2-xl", device="cuda", nodes=5, gate="bert", tp=8, pdf=True, kill_leader=False,
+            weight_dtype="fp8"),
 }
 
 TOPICS = ["raft consensus and leader election", "gradient descent for linear regression",
@@ -112,6 +113,7 @@ def main():
     ap.add_argument("--nodes", type=int)
     ap.add_argument("--device")
     ap.add_argument("--gate", choices=["bert", "off"])
+    ap.add_argument("--weight-dtype", choices=["bf16", "fp8"], help="tutor GEMM weights (config 5: fp8)")
     ap.add_argument("--gate-model", default="bert-base-uncased")
     ap.add_argument("--gate-threshold", type=float, default=0.6)
     ap.add_argument("--students", type=int, default=32)
@@ -122,7 +124,8 @@ def main():
     ap.add_argument("--startup-timeout", type=float, default=600)
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
-    for k in ("model", "tp", "nodes", "device", "gate"):
+    cfg.setdefault("weight_dtype", "bf16")
+    for k in ("model", "tp", "nodes", "device", "gate", "weight_dtype"):
         if getattr(args, k) is not None:
             cfg[k] = getattr(args, k)
 
@@ -144,6 +147,8 @@ def main():
         tut = [os.path.join(ROOT, "tutoring_server.py"), "--model", cfg["model"], "--device", cfg["device"],
                "--port", str(tutor_port), "--host", "127.0.0.1", "--max-length", str(args.max_length),
                "--max-batch", str(args.max_batch), "--log-level", "WARNING"]
+        if cfg["device"] != "cpu":
+            tut += ["--weight-dtype", cfg["weight_dtype"]]
         if cfg["tp"] > 1:
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={cfg['tp']}",
                    "--master-addr=127.0.0.1", f"--master-port={master_port}"] + tut + ["--tp", str(cfg["tp"])]
