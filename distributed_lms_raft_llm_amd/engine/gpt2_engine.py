@@ -107,13 +107,18 @@ class HipGPT2Engine:
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
                  check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16",
-                 overlap: bool | None = None, overlap_min_batch: int = 1024, overlap_parts: int | None = None):
+                 overlap: bool | None = None, overlap_min_batch: int = 1024, overlap_parts: int | None = None,
+                 p2p: bool | None = None):
         """``weight_dtype="fp8"``: W8A8 OCP-e4m3 MFMA GEMMs for QKV, c_fc and the LM head (activation
         rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path.
         ``overlap``: decode batches of >= ``overlap_min_batch`` rows run as ``overlap_parts`` row
         ranges on as many streams (attention of one beside the GEMMs of the others); default from
         ``DLMS_OVERLAP`` (on unless "0"; measured +1.7 % at 1024 queries, +7 % at 2048, 4 parts
-        and the serialised-halves schedule slower -- profiles/r1_overlap_ab.jsonl)."""
+        and the serialised-halves schedule slower -- profiles/r1_overlap_ab.jsonl).
+        ``p2p`` (TP only): the row-parallel all-reduces and the argmax-key all-gather run as
+        one-shot xGMI peer-memory kernels (``parallel/xgmi.py``) instead of RCCL calls; default
+        on for an RCCL group unless ``DLMS_XGMI=0``.  Messages larger than the slab (big packed
+        prefills) still go through RCCL."""
         if not torch.cuda.is_available():
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
@@ -157,6 +162,17 @@ class HipGPT2Engine:
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self._alloc_state()
+        self.xgmi = None
+        if self.tp_size > 1:
+            import torch.distributed as dist
+
+            if p2p is None:
+                p2p = dist.get_backend(tp_group) == "nccl" and os.environ.get("DLMS_XGMI", "1") != "0"
+            if p2p:
+                from ..parallel.xgmi import XgmiComm
+
+                slab = max(self.max_batch * cfg.n_embd * 4, 32 << 20)
+                self.xgmi = XgmiComm(tp_group, self.device, slab)
 
     # ------------------------------------------------------------------ state
     def _alloc_state(self):
@@ -200,7 +216,10 @@ class HipGPT2Engine:
         if self.tp_size > 1:
             import torch.distributed as dist
 
-            dist.all_reduce(t, group=self.tp_group)
+            if self.xgmi is not None and self.xgmi.fits(t):
+                self.xgmi.all_reduce_(t)
+            else:
+                dist.all_reduce(t, group=self.tp_group)
 
     def _gather_keys(self, B: int) -> torch.Tensor:
         """Argmax keys as a [B, P] view: the LM head's per-tile partials (TP=1), or one reduced key
@@ -210,7 +229,9 @@ class HipGPT2Engine:
 
             ops.argmax_reduce(self.key_parts[:B], out=self.local_keys[:B])
             flat = self.all_keys.view(-1)[: self.tp_size * B]
-            if dist.get_backend(self.tp_group) == "nccl":
+            if self.xgmi is not None:
+                self.xgmi.all_gather_u64(self.local_keys[:B], flat.view(self.tp_size, B))
+            elif dist.get_backend(self.tp_group) == "nccl":
                 dist.all_gather_into_tensor(flat, self.local_keys[:B], group=self.tp_group)
             else:  # gloo (functional TP tests on one GPU): list all-gather, eager only
                 parts = list(flat.view(self.tp_size, B).unbind(0))
@@ -658,6 +679,8 @@ class HipGPT2Engine:
         ev2.record()
         lens = self.lens[:n].cpu().tolist()
         toks = self.out_tokens[:n].cpu().tolist()  # one conversion, not one per row
+        if self.xgmi is not None:
+            self.xgmi.check()  # a timed-out peer barrier means these tokens are garbage
         res = [toks[b][: lens[b]] for b in range(n)]
         if stats is not None:
             ev2.synchronize()

@@ -25,7 +25,7 @@ _HERE = Path(__file__).resolve().parent
 CSRC = _HERE / "csrc"
 LIB_DIR = _HERE / "_lib"
 LIB_PATH = LIB_DIR / "libdlms_hip.so"
-SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip"]
+SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
 EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
@@ -83,6 +83,15 @@ class GemmEpi(ctypes.Structure):
     ]
 
 
+XGMI_MAX_RANKS = 8
+
+
+class XgmiArgs(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p * XGMI_MAX_RANKS), ("inp", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("n", ctypes.c_longlong), ("slab_bytes", ctypes.c_longlong), ("rank", ctypes.c_int),
+                ("world", ctypes.c_int)]
+
+
 def _bind(L):
     P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
     sig = {
@@ -108,6 +117,21 @@ def _bind(L):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    # one-shot xGMI collectives (xgmi.hip) and the IPC handle plumbing behind them
+    for name, args in {"dlms_xgmi_alloc": [ctypes.c_longlong, I, ctypes.POINTER(ctypes.c_void_p)],
+                       "dlms_xgmi_free": [P], "dlms_ipc_get_handle": [P, P],
+                       "dlms_ipc_open": [P, ctypes.POINTER(ctypes.c_void_p)], "dlms_ipc_close": [P],
+                       "dlms_xgmi_error": [P, I, ctypes.POINTER(ctypes.c_uint)],
+                       "dlms_xgmi_allreduce_f32": [ctypes.POINTER(XgmiArgs), P],
+                       "dlms_xgmi_allgather_u64": [ctypes.POINTER(XgmiArgs), P]}.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    L.dlms_xgmi_header_bytes.restype = ctypes.c_longlong
+    for name in ("dlms_ipc_handle_size", "dlms_xgmi_args_size", "dlms_xgmi_max_blocks"):
+        getattr(L, name).restype = ctypes.c_int
+    if L.dlms_xgmi_args_size() != ctypes.sizeof(XgmiArgs):
+        raise RuntimeError("XgmiArgs ABI mismatch between ctypes mirror and compiled library")
     L.dlms_gemm_force_tile.argtypes = [ctypes.c_int]
     L.dlms_gemm_force_tile.restype = None
     L.dlms_attention_variant.argtypes = [ctypes.c_int]

@@ -33,7 +33,7 @@ def _setup():
     return cfg, w, prompts
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, p2p=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -41,15 +41,18 @@ def _worker(rank, world, port, q):
         from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
         cfg, w, prompts = _setup()
-        eng = HipGPT2Engine(cfg, w, max_batch=4, max_length=64, tp_group=dist.group.WORLD, use_graph=False)
+        # p2p: one-shot xGMI kernels instead of gloo calls -- all on the GPU, so hipGraph capture works
+        eng = HipGPT2Engine(cfg, w, max_batch=4, max_length=64, tp_group=dist.group.WORLD, use_graph=p2p, p2p=p2p)
+        assert (eng.xgmi is not None) == p2p
         hid = eng.prefill_last_hidden(prompts).cpu()
         out = eng.generate(prompts)
-        q.put((rank, eng.w.head_range, hid, out))
+        q.put((rank, eng.w.head_range, hid.numpy(), out))
     finally:
         dist.destroy_process_group()
 
 
-def test_tp2_on_one_gpu_matches_tp1():
+@pytest.mark.parametrize("p2p", [False, True], ids=["gloo", "xgmi-graph"])
+def test_tp2_on_one_gpu_matches_tp1(p2p):
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
     cfg, w, prompts = _setup()
@@ -61,14 +64,14 @@ def test_tp2_on_one_gpu_matches_tp1():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, p2p)) for r in range(2)]
     [p.start() for p in procs]
     res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda r: r[0])
     [p.join(timeout=60) for p in procs]
     assert all(p.exitcode == 0 for p in procs)
     assert [r[1] for r in res] == [(0, 3), (3, 5)]
     for r in res:
-        cos = torch.nn.functional.cosine_similarity(r[2], ref_hid, dim=-1)
+        cos = torch.nn.functional.cosine_similarity(torch.from_numpy(r[2]), ref_hid, dim=-1)
         assert bool((cos > 0.999).all()), cos
         assert r[3] == res[0][3]
     agree = [sum(a == b for a, b in zip(x, y)) / max(len(x), 1) for x, y in zip(res[0][3], ref_out)]
