@@ -171,7 +171,7 @@ class HipGPT2Engine:
             if p2p:
                 from ..parallel.xgmi import XgmiComm
 
-                slab = max(self.max_batch * cfg.n_embd * 4, 32 << 20)
+                slab = max(self.max_batch * cfg.n_embd * 4, 1 << 20)  # decode messages; big prefills: RCCL
                 self.xgmi = XgmiComm(tp_group, self.device, slab)
 
     # ------------------------------------------------------------------ state

@@ -25,6 +25,12 @@ _HERE = Path(__file__).resolve().parent
 CSRC = _HERE / "csrc"
 LIB_DIR = _HERE / "_lib"
 LIB_PATH = LIB_DIR / "libdlms_hip.so"
+# debug variant: device-side range checks on every data-dependent index (common.h, DLMS_DEVICE_CHECKS)
+CHECKED_LIB_PATH = LIB_DIR / "libdlms_hip_checked.so"
+CHECK_UNITS = ("gemm", "attention", "decode", "encoder")
+CHECK_SITES = {1: "embed token id", 2: "position id", 3: "decode_update slot_map", 4: "decode_update token id",
+               5: "decode_update sequence length", 6: "seen_set row", 7: "QKV scatter slot", 8: "QKV scatter position",
+               9: "attention slot", 10: "BERT token id", 11: "seen_set token id"}
 SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
@@ -38,30 +44,39 @@ def _sources() -> list[Path]:
     return [CSRC / s for s in SOURCES]
 
 
-def needs_build() -> bool:
-    if not LIB_PATH.exists():
+def checked_mode() -> bool:
+    """``DLMS_KERNEL_CHECKS=1`` loads the range-checked debug build instead of the production one."""
+    return os.environ.get("DLMS_KERNEL_CHECKS", "0") not in ("", "0")
+
+
+def needs_build(checked: bool = False) -> bool:
+    path = CHECKED_LIB_PATH if checked else LIB_PATH
+    if not path.exists():
         return True
-    t = LIB_PATH.stat().st_mtime
+    t = path.stat().st_mtime
     deps = _sources() + list(CSRC.glob("*.h"))
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile every kernel source for gfx950 into the in-tree shared library."""
-    if not force and not needs_build():
-        return LIB_PATH
+def build(force: bool = False, verbose: bool = False, checked: bool = False) -> Path:
+    """Compile every kernel source for gfx950 into the in-tree shared library (``checked``: the
+    debug variant with device-side index range checks, ``-DDLMS_DEVICE_CHECKS=1``)."""
+    path = CHECKED_LIB_PATH if checked else LIB_PATH
+    if not force and not needs_build(checked):
+        return path
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = LIB_PATH.with_suffix(f".so.tmp{os.getpid()}")
+    tmp = path.with_suffix(f".so.tmp{os.getpid()}")
     cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
-           "-Wno-unused-result", "-o", str(tmp)] + [str(s) for s in _sources()]
+           "-Wno-unused-result"] + (["-DDLMS_DEVICE_CHECKS=1"] if checked else []) + ["-o", str(tmp)] + \
+        [str(s) for s in _sources()]
     if verbose:
         print(" ".join(cmd))
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, path)
+    return path
 
 
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), not the MI300 fnuz variant
@@ -80,6 +95,7 @@ class GemmEpi(ctypes.Structure):
         ("penalty", ctypes.c_float),
         ("split_k", ctypes.c_int), ("split_stride", ctypes.c_longlong),
         ("a_scale", ctypes.c_void_p), ("w_scale", ctypes.c_void_p),
+        ("n_slots", ctypes.c_int),
     ]
 
 
@@ -101,15 +117,15 @@ def _bind(L):
         "dlms_layernorm_gather": [P, I, P, P, P, P, I, I, I, F, P],
         "dlms_add_layernorm": [P, I, P, I, ctypes.c_longlong, I, P, P, P, P, I, P, I, P, I, I, F, I, P],
         "dlms_quantize_rows_fp8": [P, I, P, I, P, I, I, P],
-        "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
-        "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, F, P],
-        "dlms_tile_attention": [P, I, P, P, P, P, P, I, P, I, I, I, F, P],
-        "dlms_embed": [P, P, P, P, P, I, I, I, P],
+        "dlms_row_attention": [P, I, P, P, P, P, P, I, I, I, I, I, F, P],
+        "dlms_attention": [P, I, P, P, P, P, P, I, I, I, I, I, F, P],
+        "dlms_tile_attention": [P, I, P, P, P, P, P, I, P, I, I, I, I, F, P],
+        "dlms_embed": [P, P, P, P, P, I, I, I, I, I, P],
         "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I,
-                               I, I, I, P],
+                               I, I, I, I, I, P],
         "dlms_argmax_reduce": [P, I, ctypes.c_longlong, P, I, P],
-        "dlms_seen_set": [P, P, I, P, I, P],
-        "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
+        "dlms_seen_set": [P, P, I, P, I, I, P],
+        "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, I, I, P],
         "dlms_mean_pool": [P, P, P, P, I, I, P],
         "dlms_cosine": [P, P, P, I, I, I, F, P],
     }
@@ -130,6 +146,10 @@ def _bind(L):
     L.dlms_xgmi_header_bytes.restype = ctypes.c_longlong
     for name in ("dlms_ipc_handle_size", "dlms_xgmi_args_size", "dlms_xgmi_max_blocks"):
         getattr(L, name).restype = ctypes.c_int
+    for unit in CHECK_UNITS:
+        fn = getattr(L, f"dlms_check_{unit}")
+        fn.argtypes = [I, ctypes.c_void_p]
+        fn.restype = ctypes.c_int
     if L.dlms_xgmi_args_size() != ctypes.sizeof(XgmiArgs):
         raise RuntimeError("XgmiArgs ABI mismatch between ctypes mirror and compiled library")
     L.dlms_gemm_force_tile.argtypes = [ctypes.c_int]
@@ -155,12 +175,38 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            if needs_build():
-                build()
-            L = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+            checked = checked_mode()
+            if needs_build(checked):
+                build(checked=checked)
+            L = ctypes.CDLL(str(CHECKED_LIB_PATH if checked else LIB_PATH), mode=ctypes.RTLD_GLOBAL)
             _bind(L)
             _lib = L
     return _lib
+
+
+class DlmsCheckRecord(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint), ("site", ctypes.c_int), ("value", ctypes.c_longlong),
+                ("bound", ctypes.c_longlong)]
+
+
+def device_errors(clear: bool = True) -> list[str]:
+    """Index violations the checked build recorded since the last call (synchronises the device;
+    always empty with the production build, whose kernels carry no checks)."""
+    torch.cuda.synchronize()
+    out = []
+    for unit in CHECK_UNITS:
+        rec = DlmsCheckRecord()
+        _check(getattr(lib(), f"dlms_check_{unit}")(int(clear), ctypes.byref(rec)), f"dlms_check_{unit}")
+        if rec.count:
+            out.append(f"{unit}: {rec.count} out-of-range index(es); first: "
+                       f"{CHECK_SITES.get(rec.site, rec.site)} = {rec.value} not in [0, {rec.bound})")
+    return out
+
+
+def raise_on_device_errors():
+    errs = device_errors()
+    if errs:
+        raise RuntimeError("kernel index checks failed: " + "; ".join(errs))
 
 
 def available() -> bool:
@@ -255,6 +301,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
         ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
         ep.n_heads, ep.t_max, ep.d_local = k_cache.shape[1], k_cache.shape[2], d_local
+        ep.n_slots = k_cache.shape[0]
         out = q_out
     elif epi == EPI_PARTIAL:
         if split_k < 1 or K % ((128 if fp8 else 64) * split_k):
@@ -426,7 +473,7 @@ def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
     sc = (1.0 / 8.0) if scale is None else scale
     fn = lib().dlms_attention if impl == "wave" else lib().dlms_row_attention
     _check(fn(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen), _p(out), out.stride(0), R, H,
-              T, float(sc), _stream()), "attention")
+              T, S, float(sc), _stream()), "attention")
     return out
 
 
@@ -477,7 +524,8 @@ def tile_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor
         raise ValueError("tile_attention: rows must be 16-byte aligned")
     sc = (1.0 / 8.0) if scale is None else scale
     _check(lib().dlms_tile_attention(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
-                                     _p(tiles.t), tiles.n, _p(out), out.stride(0), H, T, float(sc), _stream()),
+                                     _p(tiles.t), tiles.n, _p(out), out.stride(0), H, T, k_cache.shape[0], float(sc),
+                                     _stream()),
            "tile_attention")
     return out
 
@@ -491,7 +539,8 @@ def embed(tokens: torch.Tensor, positions: torch.Tensor, wte: torch.Tensor, wpe:
     if out is None:
         out = torch.empty(R, D, dtype=torch.float32, device=tokens.device)
     _req(out, torch.float32, "out", 2)
-    _check(lib().dlms_embed(_p(tokens), _p(positions), _p(wte), _p(wpe), _p(out), out.stride(0), R, D, _stream()),
+    _check(lib().dlms_embed(_p(tokens), _p(positions), _p(wte), _p(wpe), _p(out), out.stride(0), R, D, wte.shape[0],
+                            wpe.shape[0], _stream()),
            "dlms_embed")
     return out
 
@@ -521,7 +570,8 @@ def seen_set(seen: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor):
         raise ValueError("seen_set: one row per token, contiguous bitmap")
     if R == 0:
         return seen
-    _check(lib().dlms_seen_set(_p(tokens), _p(rows), R, _p(seen), seen.shape[1], _stream()), "dlms_seen_set")
+    _check(lib().dlms_seen_set(_p(tokens), _p(rows), R, _p(seen), seen.shape[1], seen.shape[0], _stream()),
+           "dlms_seen_set")
     return seen
 
 
@@ -553,7 +603,8 @@ def decode_update(keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok,
     _check(lib().dlms_decode_update(_p(keys), P, keys.stride(0), keys.stride(1), _p(slot_map), _p(lens), _p(finished),
                                     _p(out_tokens),
                                     out_tokens.stride(0), _p(seen), seen.stride(0), _p(cur_tok), _p(cur_pos),
-                                    _p(cur_kvlen), _p(wte), _p(wpe), _p(x), x.stride(0), B, D, eos, t_max, _stream()),
+                                    _p(cur_kvlen), _p(wte), _p(wpe), _p(x), x.stride(0), B, D, eos, t_max,
+                                    lens.numel(), wte.shape[0], _stream()),
            "dlms_decode_update")
 
 
@@ -568,7 +619,8 @@ def bert_embed_ln(ids, positions, word, pos_emb, type0, gamma, beta, eps: float,
     if out_bf16 is None:
         out_bf16 = torch.empty(R, D, dtype=torch.bfloat16, device=ids.device)
     _check(lib().dlms_bert_embed_ln(_p(ids), _p(positions), _p(word), _p(pos_emb), _p(type0), _p(gamma), _p(beta),
-                                    _p(out_f32), _p(out_bf16), R, D, float(eps), _stream()), "dlms_bert_embed_ln")
+                                    _p(out_f32), _p(out_bf16), R, D, float(eps), word.shape[0], pos_emb.shape[0],
+                                    _stream()), "dlms_bert_embed_ln")
     return out_f32, out_bf16
 
 

@@ -14,7 +14,7 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ vc,
                                                             const int* __restrict__ row_slot,
                                                             const int* __restrict__ row_kvlen, bf16_t* out,
-                                                            int ldo, int H, int t_max, float scale) {
+                                                            int ldo, int H, int t_max, int n_slots, float scale) {
     __shared__ float sc[ATT_MAX_T];
     __shared__ float red[4][64];
     __shared__ float stat[2];
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
     const int wave = tid >> 6;
     const int kk = lane >> 3;  // key within the wave's group of 8
     const int c = lane & 7;    // 8-dim chunk of the head
-    const int slot = row_slot[r];
+    const int slot = (int)dlms_idx(row_slot[r], n_slots, CHK_ATTN_SLOT);
     int kvlen = row_kvlen[r];
     kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
 
@@ -116,14 +116,14 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                                         const int* __restrict__ row_slot,
                                                         const int* __restrict__ row_kvlen, bf16_t* out, int ldo, int H,
-                                                        int t_max, float scale_log2) {
+                                                        int t_max, int n_slots, float scale_log2) {
     const int lane = threadIdx.x & 63;
     const int h = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int r = blockIdx.y;
     if (h >= H) return;
     const int g = lane >> 3;
     const int c = lane & 7;
-    const int slot = row_slot[r];
+    const int slot = (int)dlms_idx(row_slot[r], n_slots, CHK_ATTN_SLOT);
     int kvlen = row_kvlen[r];
     kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
     const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
@@ -211,14 +211,14 @@ static int g_attn_variant = 0;
 extern "C" void dlms_attention_variant(int v) { g_attn_variant = v; }
 
 extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
-                                     const int* row_kvlen, void* out, int ldo, int R, int H, int t_max, float scale,
-                                     hipStream_t stream) {
+                                     const int* row_kvlen, void* out, int ldo, int R, int H, int t_max, int n_slots,
+                                     float scale, hipStream_t stream) {
     if (R <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
     const float scale_log2 = scale * 1.4426950408889634f;
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((H + 3) / 4, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
                            reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
-                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale_log2);
+                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, n_slots, scale_log2);
     };
     switch (g_attn_variant) {
         case 1: launch(attn_wave_kernel<8, false>); break;
@@ -231,11 +231,11 @@ extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, con
 
 extern "C" hipError_t dlms_row_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                          const int* row_kvlen, void* out, int ldo, int R, int H, int t_max,
-                                         float scale, hipStream_t stream) {
+                                         int n_slots, float scale, hipStream_t stream) {
     if (t_max > ATT_MAX_T || R <= 0 || H <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(row_attention_kernel, dim3(H, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
                        reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen,
-                       reinterpret_cast<bf16_t*>(out), ldo, H, t_max, scale);
+                       reinterpret_cast<bf16_t*>(out), ldo, H, t_max, n_slots, scale);
     return hipGetLastError();
 }
 
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void attn_tile_kernel(const bf16_t* __restrict
                                                         const int* __restrict__ row_slot,
                                                         const int* __restrict__ row_kvlen,
                                                         const int* __restrict__ tiles, bf16_t* __restrict__ out,
-                                                        int ldo, int H, int t_max, float scale_log2) {
+                                                        int ldo, int H, int t_max, int n_slots, float scale_log2) {
     __shared__ __attribute__((aligned(16))) char smem[4 * 4096];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void attn_tile_kernel(const bf16_t* __restrict
     const int qi = lane & 15;
     const int g = lane >> 4;
     const int qrow = row0 + (qi < nq ? qi : nq - 1);
-    const int slot = row_slot[row0];
+    const int slot = (int)dlms_idx(row_slot[row0], n_slots, CHK_ATTN_SLOT);
     int kvq = row_kvlen[qrow];
     kvq = kvq < 1 ? 1 : (kvq > t_max ? t_max : kvq);
     int kv_end = kvq;
@@ -396,12 +396,14 @@ __global__ __launch_bounds__(256) void attn_tile_kernel(const bf16_t* __restrict
 
 extern "C" hipError_t dlms_tile_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                           const int* row_kvlen, const int* tiles, int ntiles, void* out, int ldo, int H,
-                                          int t_max, float scale, hipStream_t stream) {
+                                          int t_max, int n_slots, float scale, hipStream_t stream) {
     if (ntiles <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
     const float scale_log2 = scale * 1.4426950408889634f;
     hipLaunchKernelGGL(attn_tile_kernel, dim3(ntiles, (H + 3) / 4), dim3(256), 0, stream,
                        reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
                        reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, tiles, reinterpret_cast<bf16_t*>(out),
-                       ldo, H, t_max, scale_log2);
+                       ldo, H, t_max, n_slots, scale_log2);
     return hipGetLastError();
 }
+
+DLMS_CHECK_EXPORT(attention)

@@ -99,6 +99,59 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     return base + orig / 8;
 }
 
+// ------------------------------------------------------------------ checked (debug) build
+// libdlms_hip_checked.so is compiled with -DDLMS_DEVICE_CHECKS=1 (ops.build(checked=True), used
+// when DLMS_KERNEL_CHECKS=1): every data-dependent index a kernel reads from a tensor (token ids,
+// positions, KV slots, sequence lengths) is range-checked on the device.  A violation is recorded
+// (first site / value / bound + a count) and the index is clamped to 0, so a bad input never
+// becomes an out-of-bounds access that could fault the GPU; the host reads the record with
+// dlms_check_<unit>() (ops.device_errors()).  The production build compiles the checks away.
+#ifndef DLMS_DEVICE_CHECKS
+#define DLMS_DEVICE_CHECKS 0
+#endif
+
+enum {
+    CHK_EMBED_TOKEN = 1, CHK_EMBED_POS = 2, CHK_UPDATE_SLOT = 3, CHK_UPDATE_TOKEN = 4, CHK_UPDATE_LEN = 5,
+    CHK_SEEN_ROW = 6, CHK_QKV_SLOT = 7, CHK_QKV_POS = 8, CHK_ATTN_SLOT = 9, CHK_BERT_TOKEN = 10,
+    CHK_SEEN_TOKEN = 11,
+};
+
+struct DlmsCheckRecord {
+    unsigned int count;
+    int site;
+    long long value;
+    long long bound;
+};
+
+// one record per translation unit (the library is built without relocatable device code)
+static __device__ DlmsCheckRecord dlms_check_rec;
+
+// v if 0 <= v < bound; otherwise (checked build) record the violation and return 0
+__device__ __forceinline__ long long dlms_idx(long long v, long long bound, int site) {
+#if DLMS_DEVICE_CHECKS
+    if (v < 0 || v >= bound) {
+        if (atomicAdd(&dlms_check_rec.count, 1u) == 0) {
+            dlms_check_rec.site = site;
+            dlms_check_rec.value = v;
+            dlms_check_rec.bound = bound;
+        }
+        return 0;
+    }
+#else
+    (void)bound;
+    (void)site;
+#endif
+    return v;
+}
+
+#define DLMS_CHECK_EXPORT(unit)                                                                     \
+    extern "C" int dlms_check_##unit(int clear, DlmsCheckRecord* out) {                             \
+        hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dlms_check_rec), sizeof(DlmsCheckRecord)); \
+        if (e != hipSuccess || !clear) return (int)e;                                               \
+        const DlmsCheckRecord zero = {0, 0, 0, 0};                                                  \
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(dlms_check_rec), &zero, sizeof(DlmsCheckRecord));  \
+    }
+
 // Epilogue parameters of the MFMA GEMM (gemm.hip).  Mirrored field-for-field by the ctypes
 // binding (ops/__init__.py); dlms_gemm_epi_size() lets Python assert the layouts agree.
 struct GemmEpi {
@@ -131,4 +184,5 @@ struct GemmEpi {
     // fp8 inputs (dlms_gemm_fp8): per-row activation and per-output-channel weight scales
     const float* a_scale;
     const float* w_scale;
+    int n_slots;  // EPI_QKV: KV-cache slots (the checked build range-checks row_slot against it)
 };

@@ -6,12 +6,12 @@
 // x[r] = wte[tokens[r]] + wpe[positions[r]]   (bf16 tables, f32 residual stream).  Wave per row.
 __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ tokens, const int* __restrict__ positions,
                                                     const bf16_t* __restrict__ wte, const bf16_t* __restrict__ wpe,
-                                                    float* x, int ldx, int R, int D) {
+                                                    float* x, int ldx, int R, int D, int V, int P) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
-    const bf16_t* a = wte + (size_t)tokens[r] * D;
-    const bf16_t* b = wpe + (size_t)positions[r] * D;
+    const bf16_t* a = wte + (size_t)dlms_idx(tokens[r], V, CHK_EMBED_TOKEN) * D;
+    const bf16_t* b = wpe + (size_t)dlms_idx(positions[r], P, CHK_EMBED_POS) * D;
     float* o = x + (size_t)r * ldx;
     for (int c = lane; c < D / 8; c += 64) {
         float fa[8], fb[8];
@@ -67,26 +67,28 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
                                                             int* cur_pos, int* cur_kvlen,
                                                             const bf16_t* __restrict__ wte,
                                                             const bf16_t* __restrict__ wpe, float* x, int ldx, int B,
-                                                            int D, int eos, int t_max) {
+                                                            int D, int eos, int t_max, int n_slots, int V) {
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= B) return;
     const unsigned long long best = wave_key_max(keys, i, nparts, sb, sp, lane);
-    const int b = slot_map ? slot_map[i] : i;
+    const int b = slot_map ? (int)dlms_idx(slot_map[i], n_slots, CHK_UPDATE_SLOT) : i;
     int tok = 0, pos = 0;
     if (lane == 0) {
-        int len = lens[b];
+        int len = (int)dlms_idx(lens[b], max_len + 1, CHK_UPDATE_LEN);
         if (!finished[b]) {
             // best == 0 means no shard produced a candidate (cannot happen for vocab >= 1); stay in
             // bounds anyway by emitting EOS.
             tok = best ? (int)(~(unsigned int)(best & 0xffffffffull)) : eos;
+            tok = (int)dlms_idx(tok, V, CHK_UPDATE_TOKEN);
+            len = (int)dlms_idx(len, max_len, CHK_UPDATE_LEN);
             out_tokens[(size_t)b * max_len + len] = tok;
             seen[(size_t)b * seen_words + (tok >> 5)] |= 1u << (tok & 31);
             len += 1;
             lens[b] = len;
             if (tok == eos || len >= max_len) finished[b] = 1;
         } else {
-            tok = out_tokens[(size_t)b * max_len + (len - 1)];
+            tok = (int)dlms_idx(out_tokens[(size_t)b * max_len + (len > 0 ? len - 1 : 0)], V, CHK_UPDATE_TOKEN);
         }
         pos = len - 1;
         pos = pos < t_max - 1 ? pos : t_max - 1;
@@ -109,10 +111,10 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
 }
 
 extern "C" hipError_t dlms_embed(const int* tokens, const int* positions, const void* wte, const void* wpe, float* x,
-                                 int ldx, int R, int D, hipStream_t stream) {
+                                 int ldx, int R, int D, int V, int P, hipStream_t stream) {
     if (D % 8 != 0 || R <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(embed_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, tokens, positions,
-                       reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, R, D);
+                       reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, R, D, V, P);
     return hipGetLastError();
 }
 
@@ -120,12 +122,12 @@ extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int npa
                                          const int* slot_map, int* lens, int* finished, int* out_tokens, int max_len,
                                          unsigned int* seen, int seen_words, int* cur_tok, int* cur_pos,
                                          int* cur_kvlen, const void* wte, const void* wpe, float* x, int ldx, int B,
-                                         int D, int eos, int t_max, hipStream_t stream) {
+                                         int D, int eos, int t_max, int n_slots, int V, hipStream_t stream) {
     if (D % 8 != 0 || B <= 0 || nparts <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, sp, slot_map,
                        lens, finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
                        reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, B, D, eos,
-                       t_max);
+                       t_max, n_slots, V);
     return hipGetLastError();
 }
 
@@ -140,17 +142,24 @@ extern "C" hipError_t dlms_argmax_reduce(const unsigned long long* keys, int npa
 // sequence's seen bitmap (rows pre-zeroed by the caller).  One thread per packed prompt token;
 // duplicate tokens of a row OR the same bit, so the result does not depend on the order.
 __global__ __launch_bounds__(256) void seen_set_kernel(const int* __restrict__ tokens, const int* __restrict__ rows,
-                                                       int R, unsigned int* seen, int seen_words) {
+                                                       int R, unsigned int* seen, int seen_words, int n_rows) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= R) return;
     const int t = tokens[i];
-    if (t < 0 || (t >> 5) >= seen_words) return;  // the host validates ids; never write out of the row
-    atomicOr(seen + (size_t)rows[i] * seen_words + (t >> 5), 1u << (t & 31));
+    if (t < 0 || (t >> 5) >= seen_words) {  // the host validates ids; never write out of the row
+        dlms_idx(t, (long long)seen_words * 32, CHK_SEEN_TOKEN);
+        return;
+    }
+    const size_t row = dlms_idx(rows[i], n_rows, CHK_SEEN_ROW);
+    atomicOr(seen + row * seen_words + (t >> 5), 1u << (t & 31));
 }
 
 extern "C" hipError_t dlms_seen_set(const int* tokens, const int* rows, int R, unsigned int* seen, int seen_words,
-                                    hipStream_t stream) {
+                                    int n_rows, hipStream_t stream) {
     if (R <= 0 || seen_words <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(seen_set_kernel, dim3((R + 255) / 256), dim3(256), 0, stream, tokens, rows, R, seen, seen_words);
+    hipLaunchKernelGGL(seen_set_kernel, dim3((R + 255) / 256), dim3(256), 0, stream, tokens, rows, R, seen, seen_words,
+                       n_rows);
     return hipGetLastError();
 }
+
+DLMS_CHECK_EXPORT(decode)

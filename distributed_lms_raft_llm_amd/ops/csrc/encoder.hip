@@ -12,13 +12,13 @@ __global__ __launch_bounds__(256) void bert_embed_ln_kernel(const int* __restric
                                                             const float* __restrict__ type0,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, float* out_f32,
-                                                            bf16_t* out_bf16, int R, int D, float eps) {
+                                                            bf16_t* out_bf16, int R, int D, float eps, int V, int P) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
     const int nv = D >> 2;
-    const float4* a = reinterpret_cast<const float4*>(word + (size_t)ids[r] * D);
-    const float4* p = reinterpret_cast<const float4*>(pos_emb + (size_t)positions[r] * D);
+    const float4* a = reinterpret_cast<const float4*>(word + (size_t)dlms_idx(ids[r], V, CHK_BERT_TOKEN) * D);
+    const float4* p = reinterpret_cast<const float4*>(pos_emb + (size_t)dlms_idx(positions[r], P, CHK_EMBED_POS) * D);
     const float4* t = reinterpret_cast<const float4*>(type0);
     float4 v[BE_MAX_V4];
     float s = 0.f;
@@ -98,10 +98,10 @@ __global__ __launch_bounds__(64) void cosine_kernel(const float* __restrict__ a,
 
 extern "C" hipError_t dlms_bert_embed_ln(const int* ids, const int* positions, const float* word, const float* pos_emb,
                                          const float* type0, const float* gamma, const float* beta, float* out_f32,
-                                         void* out_bf16, int R, int D, float eps, hipStream_t stream) {
+                                         void* out_bf16, int R, int D, float eps, int V, int P, hipStream_t stream) {
     if (D % 4 != 0 || D > 64 * 4 * BE_MAX_V4 || R <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(bert_embed_ln_kernel, dim3((R + 3) / 4), dim3(256), 0, stream, ids, positions, word, pos_emb,
-                       type0, gamma, beta, out_f32, reinterpret_cast<bf16_t*>(out_bf16), R, D, eps);
+                       type0, gamma, beta, out_f32, reinterpret_cast<bf16_t*>(out_bf16), R, D, eps, V, P);
     return hipGetLastError();
 }
 
@@ -118,3 +118,5 @@ extern "C" hipError_t dlms_cosine(const float* a, const float* b, float* out, in
     hipLaunchKernelGGL(cosine_kernel, dim3(NB, NA), dim3(64), 0, stream, a, b, out, NB, D, eps);
     return hipGetLastError();
 }
+
+DLMS_CHECK_EXPORT(encoder)

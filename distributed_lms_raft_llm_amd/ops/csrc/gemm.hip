@@ -317,8 +317,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
                     dst = ep.q_out + (size_t)row * ep.ldq + within;
                 } else {
                     const int head = within >> 6, dim = within & 63;
-                    dst = (part == 1 ? ep.k_cache : ep.v_cache) +
-                          (((size_t)ep.row_slot[row] * ep.n_heads + head) * ep.t_max + ep.row_pos[row]) * 64 + dim;
+                    const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
+                    const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
+                    dst = (part == 1 ? ep.k_cache : ep.v_cache) + ((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim;
                 }
                 *reinterpret_cast<uint4*>(dst) = val;
             } else {
@@ -359,8 +360,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
                         ep.q_out[(size_t)row * ep.ldq + within] = hv;
                     } else {
                         const int head = within >> 6, dim = within & 63;
-                        const size_t idx =
-                            (((size_t)ep.row_slot[row] * ep.n_heads + head) * ep.t_max + ep.row_pos[row]) * 64 + dim;
+                        const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
+                        const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
+                        const size_t idx = ((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim;
                         (part == 1 ? ep.k_cache : ep.v_cache)[idx] = hv;
                     }
                 }
@@ -483,3 +485,5 @@ extern "C" hipError_t dlms_gemm_fp8(int epi, const void* A, int lda, const void*
         default: return hipErrorInvalidValue;
     }
 }
+
+DLMS_CHECK_EXPORT(gemm)
