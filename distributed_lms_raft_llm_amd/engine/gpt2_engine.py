@@ -94,6 +94,7 @@ class _Rows:
     ln_out: dict | None = None
     pend: tuple = (None, 0, None)
     tiles: "ops.AttnTiles | None" = None  # packed prompts: MFMA tile attention instead of per-row
+    split_cap: int = 8  # split-K cap of the row-parallel projections (lower for concurrent row parts)
 
 
 def _bucket(n: int) -> int:
@@ -155,6 +156,12 @@ class HipGPT2Engine:
             overlap = os.environ.get("DLMS_OVERLAP", "1") != "0"
         self.overlap = bool(overlap)
         self.overlap_min_batch = max(2, int(overlap_min_batch))
+        # split-K cap of the row-parallel projections when row parts run concurrently: in situ at 1024
+        # queries, cap 2 beats the isolated-kernel heuristic's 4-8 slices by 4-6 % (fewer partial
+        # slabs for the add+LayerNorm to re-read while the other part streams its KV cache); single-
+        # stream batches keep the heuristic (cap 2 costs 3 % at 256, 8 % at 64).
+        # profiles/r1_split_cap_insitu.log; DLMS_OVERLAP_SPLIT_CAP overrides.
+        self.overlap_split_cap = int(os.environ.get("DLMS_OVERLAP_SPLIT_CAP", "2"))
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
         if self.overlap_parts not in (2, 3, 4):
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
@@ -242,7 +249,7 @@ class HipGPT2Engine:
         return self.key_parts[:B]
 
     # ------------------------------------------------------------------ transformer body
-    def _split(self, M: int, N: int, K: int) -> int:
+    def _split(self, M: int, N: int, K: int, cap: int = 8) -> int:
         """Split-K factor for a row-parallel projection (N = d): slice K until the grid covers the
         CUs (<= 1024 workgroups), keeping >= 3 K-steps per slice (>= 6 above M = 512, where the
         extra partial slabs the add+LayerNorm re-reads start to cost).  Fit to the cold-weight tile
@@ -256,18 +263,20 @@ class HipGPT2Engine:
         min_steps = 3 if M <= 512 else 6
         best = 1
         for s in (2, 3, 4, 6, 8):
+            if s > cap:
+                break
             if ksteps % s == 0 and tiles * s <= 1024 and ksteps // s >= min_steps:
                 best = s
         return best
 
-    def _row_parallel(self, a: torch.Tensor, w: torch.Tensor, bias, parts: torch.Tensor, M: int):
+    def _row_parallel(self, a: torch.Tensor, w: torch.Tensor, bias, parts: torch.Tensor, M: int, cap: int = 8):
         """out-proj / c_proj: split-K (TP=1) or TP partial + all-reduce.  Returns the pending
         residual update (parts, nsplit, bias) that the next fused add+LayerNorm applies."""
         if self.tp_size > 1:
             ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=1)
             self._all_reduce(parts[0, :M])
             return parts, 1, bias
-        s = self._split(M, w.shape[0], w.shape[1])
+        s = self._split(M, w.shape[0], w.shape[1], cap)
         ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=s)
         return parts, s, bias
 
@@ -304,13 +313,13 @@ class HipGPT2Engine:
     def _attn_out_mlp(self, r: "_Rows", li: int):
         """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
         lw, eps = self.w.layers[li], self.cfg.layer_norm_epsilon
-        pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M)
+        pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M, r.split_cap)
         ops.add_layernorm(r.x, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
         if self.w.fp8:
             ops.gemm(r.h8, lw.w_fc8, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff, a_scale=r.hsc, w_scale=lw.s_fc)
         else:
             ops.gemm(r.h, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff)
-        r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M)
+        r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap)
 
     def _final_ln(self, r: "_Rows", final_h: torch.Tensor | None):
         w, eps, pend = self.w, self.cfg.layer_norm_epsilon, r.pend
@@ -370,9 +379,11 @@ class HipGPT2Engine:
 
     def _part_rows(self, lo: int, hi: int) -> "_Rows":
         fp8 = self.w.fp8
-        return self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
+        r = self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
                           self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], hi - lo,
                           self.h8[lo:hi] if fp8 else None, self.hsc[lo:hi] if fp8 else None)
+        r.split_cap = self.overlap_split_cap
+        return r
 
     def _part_step(self, r: "_Rows", lo: int, penalty: float):
         """The whole decode step for one row range (rows are independent sequences)."""

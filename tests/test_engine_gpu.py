@@ -85,6 +85,9 @@ def test_overlapped_multi_stream_step_equals_serial(use_graph, parts, serial, mo
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
     monkeypatch.setenv("DLMS_OVERLAP_SERIAL", "1" if serial else "0")
+    # same split-K as the single-stream step, so the sums (and tokens) must be bit-identical; the
+    # production cap for concurrent parts (2) changes the summation order: see the test below
+    monkeypatch.setenv("DLMS_OVERLAP_SPLIT_CAP", "8")
     cfg, w = _setup("gpt2")
     prompts = _prompts(cfg, [32] * 6 + [9, 17, 3, 25], seed=5)
     ov = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=True, overlap_min_batch=2,
@@ -93,6 +96,21 @@ def test_overlapped_multi_stream_step_equals_serial(use_graph, parts, serial, mo
     a = ov.generate(prompts)
     b = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, use_graph=use_graph, overlap=False).generate(prompts)
     assert a == b
+
+
+def test_overlap_split_cap_tracks_serial():
+    """With the production split-K cap for concurrent row parts only the fp32 summation order of
+    the row-parallel partials changes: the greedy tokens track the single-stream step."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [32] * 6 + [9, 17, 3, 25], seed=5)
+    ov = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, overlap=True, overlap_min_batch=2, overlap_parts=2)
+    assert ov.overlap_split_cap == 2
+    a = ov.generate(prompts)
+    b = HipGPT2Engine(cfg, w, max_batch=16, max_length=72, overlap=False).generate(prompts)
+    agree = [sum(x == y for x, y in zip(p, q)) / len(q) for p, q in zip(a, b)]
+    assert sum(agree) / len(agree) > 0.8, agree
 
 
 def test_continuous_batching_matches_static():
