@@ -1,0 +1,61 @@
+"""bench.py driver contract on CPU: one JSON line from rank 0 with the required keys, both as a
+single process and as 2 data-parallel ranks under torchrun (gloo), where ``value`` is the
+whole-job aggregate and the elapsed time is the max over ranks."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+pytestmark = pytest.mark.timeout(300)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_lines(out: str):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+ARGS = ["--steps", "2", "--warmup", "1", "--prompt-len", "8", "--max-length", "24", "--batch", "2"]
+
+
+def test_bench_single_process_json_line():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "bench.py", *ARGS], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    d = lines[0]
+    assert KEYS <= set(d), set(KEYS) - set(d)
+    assert d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "dp1" and d["config"]["global_batch"] == 2
+    # 2 queries x (24 - 8) new tokens per step
+    assert d["new_tokens_per_step"] == 32.0
+    assert abs(d["value"] - 32.0 * 1000 / d["ms_per_step"]) / d["value"] < 0.05
+
+
+def test_bench_two_ranks_under_torchrun():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", "bench.py", "--gpus", "2", *ARGS]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    d = lines[0]
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    assert d["new_tokens_per_step"] == 64.0  # summed over both ranks
+    assert abs(d["value"] - 64.0 * 1000 / d["ms_per_step"]) / d["value"] < 0.05
