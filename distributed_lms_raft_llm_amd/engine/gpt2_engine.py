@@ -108,14 +108,16 @@ class HipGPT2Engine:
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
                  check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16",
-                 overlap: bool | None = None, overlap_min_batch: int = 1024, overlap_parts: int | None = None,
+                 overlap: bool | None = None, overlap_min_batch: int = 512, overlap_parts: int | None = None,
                  p2p: bool | None = None):
         """``weight_dtype="fp8"``: W8A8 OCP-e4m3 MFMA GEMMs for QKV, c_fc and the LM head (activation
         rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path.
         ``overlap``: decode batches of >= ``overlap_min_batch`` rows run as ``overlap_parts`` row
         ranges on as many streams (attention of one beside the GEMMs of the others); default from
         ``DLMS_OVERLAP`` (on unless "0"; measured +1.7 % at 1024 queries, +7 % at 2048, 4 parts
-        and the serialised-halves schedule slower -- profiles/r1_overlap_ab.jsonl).
+        and the serialised-halves schedule slower -- profiles/r1_overlap_ab.jsonl; with the split-K
+        cap below, +3-4 % at 512 and -11 % at 256 -- profiles/r1_split_cap_insitu.log, hence the
+        512-row threshold, ``DLMS_OVERLAP_MIN_BATCH`` overrides).
         ``p2p`` (TP only): the row-parallel all-reduces and the argmax-key all-gather run as
         one-shot xGMI peer-memory kernels (``parallel/xgmi.py``) instead of RCCL calls; default
         on for an RCCL group unless ``DLMS_XGMI=0``.  Messages larger than the slab (big packed
@@ -155,7 +157,7 @@ class HipGPT2Engine:
         if overlap is None:
             overlap = os.environ.get("DLMS_OVERLAP", "1") != "0"
         self.overlap = bool(overlap)
-        self.overlap_min_batch = max(2, int(overlap_min_batch))
+        self.overlap_min_batch = max(2, int(os.environ.get("DLMS_OVERLAP_MIN_BATCH", overlap_min_batch)))
         # split-K cap of the row-parallel projections when row parts run concurrently: in situ at 1024
         # queries, cap 2 beats the isolated-kernel heuristic's 4-8 slices by 4-6 % (fewer partial
         # slabs for the add+LayerNorm to re-read while the other part streams its KV cache); single-
