@@ -106,6 +106,9 @@ def main():
             elif name == "lmhead":
                 variants.append(("argmax", lambda i, x=x: ops.gemm(x, ws[i % nw], ops.EPI_ARGMAX, argmax_out=keys,
                                                                    seen=seen, vocab=50257, penalty=1.2)))
+                # same GEMM with a plain bf16 logits store: the fused penalty/argmax epilogue's cost
+                variants.append(("bf16_logits", lambda i, x=x, N=N: ops.gemm(x, ws[i % nw], ops.EPI_BF16,
+                                                                             out=out_bf[:, :N])))
             else:
                 variants.append(("bf16", lambda i, x=x, N=N: ops.gemm(x, ws[i % nw], ops.EPI_BF16, out=out_bf[:, :N])))
             if args.vendor:  # hipBLASLt/rocBLAS via torch, same shapes and weight rotation (reference point)
