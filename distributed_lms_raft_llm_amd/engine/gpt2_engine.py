@@ -97,6 +97,29 @@ class _Rows:
     split_cap: int = 8  # split-K cap of the row-parallel projections (lower for concurrent row parts)
 
 
+class HostResult:
+    """A device-to-host result in flight: ``result()`` waits on the event recorded right after the
+    copies were enqueued -- not on work enqueued later on the stream."""
+
+    def __init__(self, finish, keep=()):
+        self._finish, self._keep = finish, keep
+        self._ev = None
+        if keep and torch.cuda.is_available():
+            self._ev = torch.cuda.Event()
+            self._ev.record()
+
+    def result(self):
+        if self._ev is not None:
+            self._ev.synchronize()
+        return self._finish()
+
+
+def _to_device(a: np.ndarray, dev, dtype=np.int32) -> torch.Tensor:
+    """Host array -> device through pinned memory, so the copy never blocks the host on the
+    stream (a pageable-memory copy waits for the GPU to reach it: the work queued ahead)."""
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=dtype)).pin_memory().to(dev, non_blocking=True)
+
+
 def _bucket(n: int) -> int:
     for b in (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024):
         if n <= b:
@@ -536,8 +559,7 @@ class HipGPT2Engine:
         pos_np = np.arange(R, dtype=np.int64) - np.repeat(ends - lens_np, lens_np)
         slot_np = np.repeat(np.asarray(slots, dtype=np.int64), lens_np)
         tokens_d, pos_d, slot_d, last_d, slots_d, lens_d = (
-            torch.from_numpy(a.astype(np.int32)).to(dev, non_blocking=True)
-            for a in (tok_np, pos_np, slot_np, ends - 1, np.asarray(slots), lens_np))
+            _to_device(a, dev) for a in (tok_np, pos_np, slot_np, ends - 1, np.asarray(slots), lens_np))
         fin_d = (lens_d >= T).to(torch.int32)
         # per-sequence state scattered into the chosen slots on the device
         idx = slots_d.long()
@@ -623,6 +645,32 @@ class HipGPT2Engine:
 
     def finished_flags(self, B: int) -> list[int]:
         return self.finished[:B].cpu().tolist()
+
+    def flags_async(self, B: int) -> "HostResult":
+        """``finished_flags`` as a copy in flight: enqueued behind the work issued so far, read
+        by ``result()`` without waiting for anything enqueued later (the pipelined scheduler reads
+        chunk k's flags while chunk k+1 runs)."""
+        h = torch.empty(B, dtype=torch.int32, pin_memory=True)
+        h.copy_(self.finished[:B], non_blocking=True)
+        return HostResult(lambda: h.tolist(), keep=(h,))
+
+    def collect_async(self, slots: list[int]) -> "HostResult":
+        """``collect`` as a copy in flight (finished sequences never change, so the tokens can be
+        gathered behind a later decode chunk; a slot may be re-admitted right after, the admission
+        is stream-ordered behind this copy)."""
+        if not slots:
+            return HostResult(lambda: [])
+        idx = _to_device(np.asarray(slots, dtype=np.int64), self.device)
+        lens_h = torch.empty(len(slots), dtype=torch.int32, pin_memory=True)
+        toks_h = torch.empty(len(slots), self.max_length, dtype=torch.int32, pin_memory=True)
+        lens_h.copy_(self.lens.index_select(0, idx), non_blocking=True)
+        toks_h.copy_(self.out_tokens.index_select(0, idx), non_blocking=True)
+
+        def finish():
+            lens, toks = lens_h.tolist(), toks_h.tolist()
+            return [toks[i][: lens[i]] for i in range(len(slots))]
+
+        return HostResult(finish, keep=(lens_h, toks_h, idx))
 
     def collect(self, slots: list[int]) -> list[list[int]]:
         """Token sequences (prompt + generated) of ``slots``."""

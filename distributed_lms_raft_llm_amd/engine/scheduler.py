@@ -9,12 +9,20 @@ decode chunks over the smallest batch bucket covering the occupied slots, and a 
 sequence frees its slot at the next chunk boundary -- so a late request never waits for an
 earlier batch to drain.
 
+The loop is PIPELINED one chunk deep: chunk k+1 is enqueued before the host reads chunk k's stop
+flags (a pinned copy behind chunk k, ``flags_async``), and finished sequences are gathered by a
+copy enqueued behind chunk k+1 (``collect_async``: a finished row never changes), so the GPU
+always has the next chunk queued while the host retires requests and prepares admissions (the
+admission's host->device copies go through pinned memory and never block on the stream).  A
+finished slot is reusable at once: its re-admission is stream-ordered behind the gather.
+
 Engine protocol (``HipGPT2Engine`` implements it; tests use a CPU fake):
     max_batch, max_length, cfg.eos_token_id
     admit(prompts, slots, repetition_penalty)   prefill + first token into those slots
     decode(B, steps, repetition_penalty)        ``steps`` decode steps over slots [0, B)
     finished_flags(B) -> list[int]              per-slot stop flags
     collect(slots) -> list[list[int]]           prompt + generated tokens
+    flags_async(B), collect_async(slots)        optional: the same as handles with .result()
 """
 from __future__ import annotations
 
@@ -30,6 +38,24 @@ import torch
 from ..utils.metrics import METRICS
 from ..utils.trace import TRACER, roctx_range
 from .gpt2_engine import _bucket
+
+
+class _Ready:
+    def __init__(self, value):
+        self.value = value
+
+    def result(self):
+        return self.value
+
+
+def flags_async(eng, B: int):
+    f = getattr(eng, "flags_async", None)
+    return f(B) if f is not None else _Ready(eng.finished_flags(B))
+
+
+def collect_async(eng, slots: list[int]):
+    f = getattr(eng, "collect_async", None)
+    return f(slots) if f is not None else _Ready(eng.collect(slots))
 
 
 @dataclass
@@ -111,12 +137,15 @@ class ContinuousBatcher:
 
     def _loop(self):
         eng = self.engine
+        prev = None  # (flags handle, {slot: request} live when that chunk was enqueued) of the last chunk
+        retiring = None  # (requests, collect handle) of sequences found finished
         while True:
             with self._cv:
-                while not self._stop and not self._queue and not self._active:
+                while not self._stop and not self._queue and not self._active and prev is None and retiring is None:
                     self._cv.wait()
                 if self._stop:
-                    waiters = list(self._queue) + list(self._active.values())
+                    waiters = list(self._queue) + list(self._active.values()) + \
+                        ([r for _, r in retiring[0]] if retiring else [])
                     self._queue.clear()
                     self._active.clear()
                     for r in waiters:
@@ -132,35 +161,48 @@ class ContinuousBatcher:
                     eng.admit([r.prompt for _, r in admits], [s for s, _ in admits], self.penalty)
                 TRACER.complete("tutor.admit", ta, cat="tutor", n=len(admits),
                                 tokens=sum(len(r.prompt) for _, r in admits))
-                t_first = time.perf_counter()  # prefill emitted every admitted query's first token
+                t_first = time.perf_counter()  # prefill (first token included) is enqueued
                 for s, r in admits:
                     self._active[s] = r
                     r.t_first = t_first
                     METRICS.observe(f"{self.name}_queue_ms", (ta - r.t_submit) * 1e3)
                     METRICS.observe(f"{self.name}_ttft_ms", (t_first - r.t_submit) * 1e3)
-            B = min(_bucket(max(self._active) + 1), eng.max_batch)
-            td = time.perf_counter()
-            with roctx_range("decode_chunk"):
-                eng.decode(B, self.chunk, self.penalty)
-                flags = eng.finished_flags(B)  # the sync point of the chunk
-            self.steps += self.chunk
-            TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
-                            steps=self.chunk)
-            done = [s for s in self._active if flags[s]]
-            if not done:
-                continue
-            outs = eng.collect(done)
-            now = time.perf_counter()
-            with self._cv:
-                for s, out in zip(done, outs):
-                    r = self._active.pop(s)
-                    heapq.heappush(self._free, s)
-                    self.completed += 1
-                    n_new = len(out) - len(r.prompt)
-                    METRICS.observe(f"{self.name}_request_ms", (now - r.t_submit) * 1e3)
-                    if n_new > 1:  # time per output token after the first
-                        METRICS.observe(f"{self.name}_tpot_ms", (now - r.t_first) * 1e3 / (n_new - 1))
-                    METRICS.inc(f"{self.name}_tokens", n_new)
-                    r.future.set_result(out)
-            METRICS.set(f"{self.name}_active", len(self._active))
-            METRICS.set(f"{self.name}_kv_slot_occupancy", len(self._active) / eng.max_batch)
+            cur = None
+            if self._active:
+                B = min(_bucket(max(self._active) + 1), eng.max_batch)
+                td = time.perf_counter()
+                with roctx_range("decode_chunk"):
+                    eng.decode(B, self.chunk, self.penalty)
+                    cur = (flags_async(eng, B), dict(self._active))
+                self.steps += self.chunk
+                TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
+                                steps=self.chunk)
+            if retiring is not None:  # gathered behind the chunk before `cur`: ready or nearly
+                self._retire(*retiring)
+                retiring = None
+            if prev is not None:  # chunk k's flags while chunk k+1 runs
+                flags = prev[0].result()
+                # by identity: a slot retired one chunk earlier may already hold a new request
+                done = [s for s, r in prev[1].items() if s < len(flags) and flags[s] and self._active.get(s) is r]
+                if done:
+                    handle = collect_async(eng, done)
+                    with self._cv:
+                        reqs = [(s, self._active.pop(s)) for s in done]
+                        for s in done:
+                            heapq.heappush(self._free, s)
+                    retiring = (reqs, handle)
+                    METRICS.set(f"{self.name}_active", len(self._active))
+                    METRICS.set(f"{self.name}_kv_slot_occupancy", len(self._active) / eng.max_batch)
+            prev = cur
+
+    def _retire(self, reqs, handle):
+        outs = handle.result()
+        now = time.perf_counter()
+        for (s, r), out in zip(reqs, outs):
+            self.completed += 1
+            n_new = len(out) - len(r.prompt)
+            METRICS.observe(f"{self.name}_request_ms", (now - r.t_submit) * 1e3)
+            if n_new > 1:  # time per output token after the first
+                METRICS.observe(f"{self.name}_tpot_ms", (now - r.t_first) * 1e3 / (n_new - 1))
+            METRICS.inc(f"{self.name}_tokens", n_new)
+            r.future.set_result(out)

@@ -56,6 +56,16 @@ class TPEngineProxy:
     def collect(self, slots):
         return self.engine.collect(slots)
 
+    def flags_async(self, B: int):  # rank-0 reads only: nothing to mirror
+        from .scheduler import flags_async
+
+        return flags_async(self.engine, B)
+
+    def collect_async(self, slots):
+        from .scheduler import collect_async
+
+        return collect_async(self.engine, slots)
+
     def close(self):
         """Release the followers.  Tolerates followers that are already gone (a launcher that
         signals the whole process group stops them before rank 0 gets here)."""

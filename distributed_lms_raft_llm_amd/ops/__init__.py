@@ -495,7 +495,10 @@ class AttnTiles:
         nq = np.minimum(16, lens[seq] - 16 * k)
         self.rows = int(lens.sum())
         self.n = int(nt.sum())
-        self.t = torch.from_numpy(np.stack([row0, nq], axis=1).astype(np.int32)).to(device, non_blocking=True)
+        t = torch.from_numpy(np.stack([row0, nq], axis=1).astype(np.int32))
+        if torch.device(device).type == "cuda":
+            t = t.pin_memory()  # a pageable copy would block the host until the GPU reaches it
+        self.t = t.to(device, non_blocking=True)
 
 
 def tile_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,

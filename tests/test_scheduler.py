@@ -158,3 +158,32 @@ def test_kv_capacity_planner():
     assert slot_bytes(xl, 150, 8, 0) > slot_bytes(xl, 150, 8, 7)
     with pytest.raises(MemoryError):
         plan_max_batch(small, 150, free_bytes=1 * GIB)
+
+
+class AsyncFakeEngine(FakeSlotEngine):
+    """Fake whose flags/collect are snapshots taken when requested (like the device copies the
+    pipelined loop enqueues) and read later."""
+
+    def flags_async(self, B):
+        snap = list(self.fin[:B])
+        return SimpleNamespace(result=lambda: snap)
+
+    def collect_async(self, slots):
+        snap = [list(self.seqs[s]) for s in slots]
+        return SimpleNamespace(result=lambda: snap)
+
+
+@pytest.mark.parametrize("engine_cls", [FakeSlotEngine, AsyncFakeEngine])
+def test_pipelined_loop_readmits_retired_slots_immediately(engine_cls):
+    """Two slots, chunk 1, many short requests: a slot retired from chunk k's flags is re-admitted
+    while chunk k+1's (stale) flags still call it finished -- the new request must not be retired
+    with the old one's flags."""
+    eng = engine_cls(max_batch=2, max_length=12)
+    cb = ContinuousBatcher(eng, chunk=1)
+    try:
+        prompts = _prompts(30, seed=7)
+        outs = [f.result(10) for f in [cb.submit(p) for p in prompts]]
+    finally:
+        cb.stop()
+    assert outs == [solo(p, 12) for p in prompts]
+    assert cb.completed == 30 and eng.admitted_while_busy > 0
