@@ -178,7 +178,8 @@ def lib():
             checked = checked_mode()
             if needs_build(checked):
                 build(checked=checked)
-            L = ctypes.CDLL(str(CHECKED_LIB_PATH if checked else LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+            path = os.environ.get("DLMS_HIP_LIB") or str(CHECKED_LIB_PATH if checked else LIB_PATH)
+            L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)  # DLMS_HIP_LIB: A/B builds in experiments
             _bind(L)
             _lib = L
     return _lib

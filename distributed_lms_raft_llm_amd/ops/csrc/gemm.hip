@@ -182,6 +182,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     bfr[j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frow) * ROWB + coff);
+                // (s_setprio(1)/(0) around this cluster, cdna guide T5, measured null on this 1-barrier
+                // loop: prefill shapes and the whole decode within noise)
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -428,6 +430,10 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
         }
     }
     if (N % 256 == 0 && id == 9) return launch_gemm_cfg<128, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    // 256x256, 8 waves of 128x64 (the cdna guide's big-tile geometry, on this kernel's 1-barrier loop)
+    // (not for the fp32 split-K epilogue: its 256 x 1 KiB staged rows exceed the LDS)
+    if (N % 256 == 0 && id == 14 && EPI != EPI_PARTIAL)
+        return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     *done = false;
     return hipSuccess;
 }
@@ -443,6 +449,15 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     }
     const long t64 = (long)((M + 63) / 64) * (N / 64) * split;
     const long t128 = (long)((M + 127) / 128) * (N / 128) * split;
+    // big prefill GEMMs with a bf16 epilogue: 256x256 tiles, 8 waves of 128x64 (one workgroup per
+    // CU: its 128 KiB ring + 135 KiB staged epilogue), unless the last round of tiles would run
+    // nearly empty (profiles/r1_gemm_256tile.jsonl: c_fc M=32768 247 -> 192 us, QKV 184 -> 154 us;
+    // QKV at M=8192 = 288 tiles loses 6 %)
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_QKV) {
+        const long t256 = (long)((M + 255) / 256) * (N / 256);
+        if (N % 256 == 0 && M >= 4096 && (t256 <= 256 || t256 % 256 >= 128 || t256 >= 512))
+            return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    }
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
         return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);

@@ -20,7 +20,8 @@ from distributed_lms_raft_llm_amd import ops  # noqa: E402
 
 TILES = {-1: "auto", 0: "32x64s6", 1: "64x64s4", 2: "128x64s3", 3: "128x128s3", 4: "64x64s2", 5: "64x128s3",
          6: "128x128s2", 7: "64x64s6", 8: "256x128w8s2", 9: "128x256w8s2", 10: "128x128w8s3(4x2)",
-         11: "128x128w8s3(2x4)", 12: "256x128s2(wave128x64)", 13: "256x128s3(wave128x64)"}
+         11: "128x128w8s3(2x4)", 12: "256x128s2(wave128x64)", 13: "256x128s3(wave128x64)",
+         14: "256x256w8s2(wave128x64)"}
 
 
 def graph_time(fn, inner=20, reps=15):
@@ -52,6 +53,7 @@ def graph_time(fn, inner=20, reps=15):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--d", type=int, default=768)
+    ap.add_argument("--vocab", type=int, default=50304, help="LM-head N (padded vocabulary)")
     ap.add_argument("--batches", default="64,256,512")
     ap.add_argument("--tiles", default="-1,1,2,3,4,5,7")
     ap.add_argument("--T", type=int, default=150)
@@ -66,7 +68,7 @@ def main():
     dev = "cuda"
     d = args.d
     H = d // 64
-    V = 50304
+    V = args.vocab
     tiles = [int(t) for t in args.tiles.split(",")]
     res = []
 

@@ -88,6 +88,42 @@ def test_gemm_qkv_scatter():
         torch.testing.assert_close(vc[s, :, p].float().reshape(-1), ref[m, 2 * D:], atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("epi", ["bf16", "gelu_tanh", "qkv"])
+def test_gemm_256_tiles_large_m(epi):
+    """Prefill-sized GEMMs (M >= 4096, N % 256 == 0) take the 256x256 8-wave tile: bias/GELU
+    epilogues and the QKV scatter (4096 packed rows over 4 slots x 1024 positions), vs fp32."""
+    ops = _ops()
+    M, K = 4096, 768
+    if epi == "qkv":
+        H, S = 4, 4
+        D = H * 64
+        T = M // S
+        a, w = _bf(M, K if K == D else D, seed=21), _bf(3 * D, D, scale=0.05, seed=22)
+        bias = torch.randn(3 * D, device=DEV)
+        q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+        kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros_like(kc)
+        slot = (torch.arange(M, device=DEV) // T).to(torch.int32)
+        pos = (torch.arange(M, device=DEV) % T).to(torch.int32)
+        ops.gemm(a, w, ops.EPI_QKV, bias=bias, q_out=q, k_cache=kc, v_cache=vc, row_slot=slot, row_pos=pos)
+        ref = a.float() @ w.float().t() + bias
+        torch.testing.assert_close(q.float(), ref[:, :D], atol=2e-2, rtol=2e-2)
+        # cache [S][H][T][64] -> [S*T][H*64] rows in packed order
+        k_rows = kc.permute(0, 2, 1, 3).reshape(M, D).float()
+        v_rows = vc.permute(0, 2, 1, 3).reshape(M, D).float()
+        torch.testing.assert_close(k_rows, ref[:, D:2 * D], atol=2e-2, rtol=2e-2)
+        torch.testing.assert_close(v_rows, ref[:, 2 * D:], atol=2e-2, rtol=2e-2)
+        return
+    N = 3072
+    a, w = _bf(M, K, seed=23), _bf(N, K, scale=0.05, seed=24)
+    bias = torch.randn(N, device=DEV) * 0.1
+    out = ops.gemm(a, w, ops.EPI_BF16 if epi == "bf16" else ops.EPI_GELU_TANH, bias=bias)
+    ref = a.float() @ w.float().t() + bias
+    if epi == "gelu_tanh":
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
 def test_gemm_argmax_penalty():
     ops = _ops()
     M, K, V = 37, 768, 50257
