@@ -267,7 +267,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
                 const unsigned long long o = sred[w * BM + lr];
                 b = o > b ? o : b;
             }
-            if (m0 + lr < M) ep.argmax_out[(size_t)(m0 + lr) * ep.ldo + (n0 >> 6)] = b;
+            if (m0 + lr < M) {
+                // one key per 64-column group: a BN > 64 tile also zeroes the groups it covers, so
+                // keys left by an earlier, narrower tile config can never win the consumer's max
+                unsigned long long* o = ep.argmax_out + (size_t)(m0 + lr) * ep.ldo + (n0 >> 6);
+                o[0] = b;
+#pragma unroll
+                for (int g = 1; g < BN / 64; ++g) o[g] = 0ull;
+            }
         }
         return;
     }
@@ -458,6 +465,9 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
         if (N % 256 == 0 && M >= 4096 && (t256 <= 256 || t256 % 256 >= 128 || t256 >= 512))
             return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     }
+    // (LM head on a 512-row decode half: 256x256 tiles are 86.4 -> 78.3 us alone (N = 50432,
+    // profiles/r1_gemm_256tile.jsonl) but 1 % slower in the two-stream decode step, where the
+    // one-workgroup-per-CU tile starves the other half's kernels: profiles/r1_lmhead_256_ab.log)
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
         return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);

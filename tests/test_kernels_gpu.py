@@ -124,9 +124,13 @@ def test_gemm_256_tiles_large_m(epi):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-def test_gemm_argmax_penalty():
+@pytest.mark.parametrize("M", [37, 512])
+def test_gemm_argmax_penalty(M):
+    """Fused penalty + argmax epilogue vs fp32.  The key buffer is pre-filled with huge stale keys,
+    which a tile wider than 64 columns must zero in every 64-column group it covers (a narrower
+    earlier config could have left keys there)."""
     ops = _ops()
-    M, K, V = 37, 768, 50257
+    K, V = 768, 50257
     Vp = (V + 63) // 64 * 64
     a = _bf(M, K, seed=9)
     w = torch.zeros(Vp, K, dtype=torch.bfloat16, device=DEV)
@@ -142,7 +146,7 @@ def test_gemm_argmax_penalty():
     for bit in range(32):
         words |= seen_bool.view(M, Vp // 32, 32)[:, :, bit].long() << bit
     seen.copy_(words.to(torch.int64).where(words < 2**31, words - 2**32).to(torch.int32))
-    parts = torch.zeros(M, Vp // 64, dtype=torch.int64, device=DEV)
+    parts = torch.full((M, Vp // 64), 2**62, dtype=torch.int64, device=DEV)
     ops.gemm(a, w, ops.EPI_ARGMAX, argmax_out=parts, seen=seen, vocab=V, penalty=1.2)
     keys = ops.argmax_reduce(parts)
     pen = torch.where(logits < 0, logits * 1.2, logits / 1.2)
