@@ -468,6 +468,15 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     // (LM head on a 512-row decode half: 256x256 tiles are 86.4 -> 78.3 us alone (N = 50432,
     // profiles/r1_gemm_256tile.jsonl) but 1 % slower in the two-stream decode step, where the
     // one-workgroup-per-CU tile starves the other half's kernels: profiles/r1_lmhead_256_ab.log)
+    // decode GEMMs of the wider models (K = d >= 1024: GPT-2-medium/large/XL QKV and c_fc on 256-512
+    // row halves): 128x64 tiles with a 3-deep ring while they fit in one round of workgroups
+    // (profiles/r1_gemm_wide_models.jsonl: medium M=512 c_fc 15.0 -> 11.6 us, XL M=256 QKV 17.3 ->
+    // 15.6 us / c_fc 17.8 -> 15.8 us; at 300-400 tiles 64x64 wins again)
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_QKV) {
+        const long t128x64 = (long)((M + 127) / 128) * (N / 64);
+        if (K >= 1024 && M >= 256 && t128x64 <= 256)
+            return launch_gemm_cfg<128, 64, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    }
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
         return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);

@@ -124,6 +124,35 @@ def test_gemm_256_tiles_large_m(epi):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("epi,M,N,K", [("gelu_tanh", 256, 6400, 1600), ("bf16", 300, 4096, 1024),
+                                        ("qkv", 256, 3072, 1024)])
+def test_gemm_wide_model_tiles(epi, M, N, K):
+    """Decode GEMMs of the wider GPT-2 sizes (K >= 1024, <= 256 tiles of 128x64) take the 128x64
+    3-stage tile: GELU / bias epilogues (incl. a ragged 300-row tail) and the QKV scatter, vs fp32."""
+    ops = _ops()
+    a, w = _bf(M, K, seed=31), _bf(N, K, scale=0.03, seed=32)
+    bias = torch.randn(N, device=DEV) * 0.1
+    ref = a.float() @ w.float().t() + bias
+    if epi == "qkv":
+        D = K
+        H, S = D // 64, 2
+        T = M // S
+        q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+        kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros_like(kc)
+        slot = (torch.arange(M, device=DEV) // T).to(torch.int32)
+        pos = (torch.arange(M, device=DEV) % T).to(torch.int32)
+        ops.gemm(a, w, ops.EPI_QKV, bias=bias, q_out=q, k_cache=kc, v_cache=vc, row_slot=slot, row_pos=pos)
+        torch.testing.assert_close(q.float(), ref[:, :D], atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(kc.permute(0, 2, 1, 3).reshape(M, D).float(), ref[:, D:2 * D], atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(vc.permute(0, 2, 1, 3).reshape(M, D).float(), ref[:, 2 * D:], atol=3e-2, rtol=2e-2)
+        return
+    out = ops.gemm(a, w, ops.EPI_BF16 if epi == "bf16" else ops.EPI_GELU_TANH, bias=bias)
+    if epi == "gelu_tanh":
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("M", [37, 512])
 def test_gemm_argmax_penalty(M):
     """Fused penalty + argmax epilogue vs fp32.  The key buffer is pre-filled with huge stale keys,
