@@ -41,7 +41,9 @@ def _worker(rank, world, port, q):
         prompt = torch.randint(0, CFG.vocab_size - 1, (9,), generator=g).tolist()
         hid = m.forward(torch.tensor(prompt), torch.arange(len(prompt)), m.new_cache(40))
         out = m.generate(prompt, max_length=40)
-        q.put((rank, m.w.head_range, m.w.vocab_range, hid[-1].clone(), out, prompt))
+        # numpy pickles by value: a torch tensor would go through the sender's resource-sharer socket,
+        # which is gone if this worker exits before the parent reads the queue
+        q.put((rank, m.w.head_range, m.w.vocab_range, hid[-1].detach().numpy().copy(), out, prompt))
     finally:
         dist.destroy_process_group()
 
@@ -68,7 +70,7 @@ def test_tp_matches_unsharded(world):
     hid = ref.forward(torch.tensor([prompt]), torch.arange(len(prompt))[None], KVCache.allocate(CFG, 1, 40),
                       torch.zeros(1, dtype=torch.long))[0, -1]
     for r in res:
-        torch.testing.assert_close(r[3], hid, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(torch.from_numpy(r[3]), hid, atol=1e-4, rtol=1e-4)
         assert r[4] == res[0][4]  # every rank produced the same tokens
     assert res[0][4] == reference_generate(ref, [prompt], max_length=40)[0]
 
