@@ -38,6 +38,49 @@ BASELINE_TOK_S = 53.7  # reference GPT-2-124M generate on CPU
 METRIC = "tutoring tokens/sec (GPT-2-124M) + p50 query latency at 1/2/4/8 MI355X"
 
 
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N ranks of this script as child processes (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set like torchrun) BEFORE this process touches the
+    GPU, wait for all of them and return the first non-zero exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+def latency_point(eng, cfg, B: int, prompt_len: int, max_length: int, reps: int, seed: int, gpu: bool) -> dict:
+    """p50 wall time of ``reps`` generate() calls of B concurrent queries on an otherwise idle
+    engine (after two warmup calls that capture the bucket's hipGraph), and the decode tokens/s."""
+    g = torch.Generator().manual_seed(seed)
+    prompts = torch.randint(0, cfg.vocab_size - 1, (B, prompt_len), generator=g).tolist()
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import GenerateStats
+
+    for _ in range(2):
+        eng.generate(prompts, max_length)
+    times, st = [], GenerateStats()
+    for _ in range(reps):
+        if gpu:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.generate(prompts, max_length, stats=st)
+        if gpu:
+            torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+    p50 = statistics.median(times)
+    return {f"p50_query_latency_ms_b{B}": round(p50, 3), f"tok_s_b{B}": round(st.new_tokens / (sum(times) / 1e3), 1),
+            f"prefill_ms_b{B}": round(st.prefill_ms / reps, 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -52,7 +95,14 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--weight-dtype", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = W8A8 e4m3 QKV/c_fc/LM head (not the headline: reduced precision)")
+    ap.add_argument("--latency-batches", default="1,32",
+                    help="after the timed headline: unloaded p50 latency at these batch sizes ('' = skip)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(spawn_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
 
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import GenerateStats, HipGPT2Engine, TorchGPT2Engine
     from distributed_lms_raft_llm_amd.models.config import gpt2_config
@@ -133,6 +183,12 @@ def main():
 
     tok_s = total_new / elapsed_max
     p50 = statistics.median(per_step_ms)
+    extra = {}
+    for lb in [int(b) for b in args.latency_batches.split(",") if b.strip()]:
+        if lb <= B:  # outside the timed region: the unloaded latency operating points
+            extra.update(latency_point(eng, cfg, lb, args.prompt_len, args.max_length, 5, 2000 + dp_rank, gpu))
+    if dist is not None:
+        dist.barrier()
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -150,6 +206,7 @@ def main():
             "p50_query_latency_ms": round(p50, 3),
             "baseline_p50_query_latency_ms": 2198,
             "new_tokens_per_step": total_new / args.steps,
+            **extra,
             "config": {
                 "model": f"{args.model} ({cfg.num_params() / 1e6:.0f}M)",
                 "global_batch": B * dp_size,

@@ -95,6 +95,7 @@ class _Rows:
     pend: tuple = (None, 0, None)
     tiles: "ops.AttnTiles | None" = None  # packed prompts: MFMA tile attention instead of per-row
     split_cap: int = 8  # split-K cap of the row-parallel projections (lower for concurrent row parts)
+    split_fixed: int | None = None  # pinned split-K (M-independent arithmetic: prefill_split)
 
 
 class HostResult:
@@ -128,11 +129,18 @@ def _bucket(n: int) -> int:
 
 
 class HipGPT2Engine:
+    # (row, head) pairs up to which decode attention uses the split-K kernel (profiles/r2_skinny_bench.log:
+    # at 32 rows x 12 heads, T=150: 7.9 us vs 12.3 us for one wave per pair)
+    SPLIT_ATTN_MAX_PAIRS = 1024
+    # split-K of the row-parallel projections on the latency path (fixed: the fused add+LN
+    # kernel sums exactly this many slabs)
+    SMALL_SPLIT = 4
+
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
                  check_every: int = 16, max_batch_cap: int = 4096, weight_dtype: str = "bf16",
                  overlap: bool | None = None, overlap_min_batch: int = 512, overlap_parts: int | None = None,
-                 p2p: bool | None = None):
+                 p2p: bool | None = None, latency_path: bool | None = None, prefill_split: int | None = None):
         """``weight_dtype="fp8"``: W8A8 OCP-e4m3 MFMA GEMMs for QKV, c_fc and the LM head (activation
         rows scaled by the fused LayerNorms); the bf16 default is the reference-precision path.
         ``overlap``: decode batches of >= ``overlap_min_batch`` rows run as ``overlap_parts`` row
@@ -144,7 +152,14 @@ class HipGPT2Engine:
         ``p2p`` (TP only): the row-parallel all-reduces and the argmax-key all-gather run as
         one-shot xGMI peer-memory kernels (``parallel/xgmi.py``) instead of RCCL calls; default
         on for an RCCL group unless ``DLMS_XGMI=0``.  Messages larger than the slab (big packed
-        prefills) still go through RCCL."""
+        prefills) still go through RCCL.
+        ``latency_path`` (default on unless ``DLMS_LATENCY_PATH=0``): decode buckets of at most
+        ``ops.skinny_addln_max_rows(d)`` rows (8 for GPT-2 small/medium) run the latency-shaped step
+        (``_decode_step_small``): fused add+LN+GEMM on pre-shuffled weights for LN1->QKV and
+        LN2->c_fc, split-K flash-decode attention, no standalone LayerNorm kernels.
+        ``prefill_split``: pin the split-K of the prefill's row-parallel projections (default: a
+        heuristic of the packed row count) so a prompt's arithmetic does not depend on what else is
+        admitted with it -- continuous batching is then bit-identical to serving it alone."""
         if not torch.cuda.is_available():
             raise RuntimeError("HipGPT2Engine needs a GPU (use TorchGPT2Engine on CPU)")
         ops.lib()  # fail loudly if the kernel library is missing
@@ -176,6 +191,7 @@ class HipGPT2Engine:
         self.max_batch = int(max_batch)
         self.max_length = max_length
         self.use_graph = use_graph
+        self.prefill_split = prefill_split
         self.check_every = check_every
         if overlap is None:
             overlap = os.environ.get("DLMS_OVERLAP", "1") != "0"
@@ -190,6 +206,16 @@ class HipGPT2Engine:
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
         if self.overlap_parts not in (2, 3, 4):
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
+        if latency_path is None:
+            latency_path = os.environ.get("DLMS_LATENCY_PATH", "1") != "0"
+        self.small_max = ops.skinny_addln_max_rows(cfg.n_embd) if (latency_path and not self.w.fp8) else 0
+        if self.tp_size == 1 and any((k // 64) % self.SMALL_SPLIT for k in (self.w.d_local, self.w.ffn_local)):
+            self.small_max = 0  # the fused add+LN kernel sums exactly SMALL_SPLIT slabs (tiny test models)
+        if self.small_max:
+            for lw in self.w.layers:  # MFMA-fragment-order copies of the QKV / c_fc weights
+                if lw.w_qkv_sh is None:
+                    lw.w_qkv_sh = ops.shuffle_weight(lw.w_qkv)
+                    lw.w_fc_sh = ops.shuffle_weight(lw.w_fc)
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -215,6 +241,8 @@ class HipGPT2Engine:
         # KV cache [L][2][slots][H_local][T][64]: sized for the batch at full length.
         self.kv = torch.zeros(cfg.n_layer, 2, B, Hl, T, 64, dtype=bf, device=dev)
         self.x = torch.zeros(B, D, dtype=f32, device=dev)
+        # second residual buffer: the latency path's fused add+LN kernels advance x by ping-pong
+        self.x2 = torch.zeros(min(B, 64), D, dtype=f32, device=dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
         self.h = torch.zeros(B, D, dtype=bf, device=dev)
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
@@ -294,14 +322,18 @@ class HipGPT2Engine:
                 best = s
         return best
 
-    def _row_parallel(self, a: torch.Tensor, w: torch.Tensor, bias, parts: torch.Tensor, M: int, cap: int = 8):
+    def _row_parallel(self, a: torch.Tensor, w: torch.Tensor, bias, parts: torch.Tensor, M: int, cap: int = 8,
+                      fixed: int | None = None):
         """out-proj / c_proj: split-K (TP=1) or TP partial + all-reduce.  Returns the pending
         residual update (parts, nsplit, bias) that the next fused add+LayerNorm applies."""
         if self.tp_size > 1:
             ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=1)
             self._all_reduce(parts[0, :M])
             return parts, 1, bias
-        s = self._split(M, w.shape[0], w.shape[1], cap)
+        if fixed:
+            s = max(d for d in range(1, fixed + 1) if (w.shape[1] // 64) % d == 0)
+        else:
+            s = self._split(M, w.shape[0], w.shape[1], cap)
         ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=s)
         return parts, s, bias
 
@@ -332,19 +364,23 @@ class HipGPT2Engine:
     def _attn(self, r: "_Rows", li: int):
         if r.tiles is not None:  # packed prompts (K6): 16-query MFMA tiles
             ops.tile_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, r.tiles, out=r.att)
+        elif r.M * self.w.n_heads_local <= self.SPLIT_ATTN_MAX_PAIRS:
+            # decode with few (row, head) pairs: split-K flash-decode puts NW waves on each pair's keys
+            ops.attention_split(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
+                                waves=ops.attention_split_waves(self.max_length))
         else:  # decode (K5): one query per sequence, a pure KV stream
             ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att)
 
     def _attn_out_mlp(self, r: "_Rows", li: int):
         """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
         lw, eps = self.w.layers[li], self.cfg.layer_norm_epsilon
-        pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M, r.split_cap)
+        pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M, r.split_cap, r.split_fixed)
         ops.add_layernorm(r.x, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
         if self.w.fp8:
             ops.gemm(r.h8, lw.w_fc8, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff, a_scale=r.hsc, w_scale=lw.s_fc)
         else:
             ops.gemm(r.h, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff)
-        r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap)
+        r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap, r.split_fixed)
 
     def _final_ln(self, r: "_Rows", final_h: torch.Tensor | None):
         w, eps, pend = self.w, self.cfg.layer_norm_epsilon, r.pend
@@ -363,6 +399,8 @@ class HipGPT2Engine:
         LayerNorms emit row-scaled e4m3 into ``h8``/``hsc`` for the W8A8 QKV / c_fc GEMMs, and the
         ln_f output goes there too (``final_h`` then only says whether it is wanted)."""
         r = self._rows(x, parts, h, q, att, ff, row_slot, row_pos, row_kvlen, M, h8, hsc, tiles)
+        if tiles is not None:
+            r.split_fixed = self.prefill_split
         for li in range(len(self.w.layers)):
             self._attn_in(r, li)
             self._attn(r, li)
@@ -477,7 +515,55 @@ class HipGPT2Engine:
                     if p < L:
                         self._attn(r, p)
 
+    def _small_ok(self, B: int) -> bool:
+        return 0 < B <= self.small_max
+
+    def _decode_step_small(self, B: int, penalty: float):
+        """Latency-shaped decode step for B <= ``small_max`` rows: per layer
+        [add+LN1+QKV] -> split-K attention -> out-proj (split-K partials) -> [add+LN2+c_fc+GELU]
+        -> c_proj (partials); the residual ping-pongs between ``x`` and ``x2`` (every workgroup of a
+        fused add+LN kernel re-reads its input rows, so the updated rows go to the other buffer).
+        Under TP the partial is all-reduced first and summed as one slab."""
+        eps = self.cfg.layer_norm_epsilon
+        r = self._rows(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
+                       self.cur_kvlen[:B], B)
+        bufs = (self.x[:B], self.x2[:B])
+        cur = 0
+        pend = None  # (nsplit, residual bias) still to be added into x
+        tp = self.tp_size > 1
+        split = 1 if tp else self.SMALL_SPLIT
+        parts = self.parts[:, :B]
+
+        def row_parallel(a, w):
+            ops.gemm(a, w, ops.EPI_PARTIAL, out=self.parts, split_k=split)
+            if tp:
+                self._all_reduce(self.parts[0, :B])
+            return split
+
+        for li, lw in enumerate(self.w.layers):
+            kc, vc = self.kv[li, 0], self.kv[li, 1]
+            if pend is None:
+                ops.skinny_addln_gemm(bufs[cur], lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, bias=lw.b_qkv,
+                                      q_out=r.q, k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
+            else:
+                ops.skinny_addln_gemm(bufs[cur], lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, x_out=bufs[1 - cur],
+                                      parts=parts, nsplit=pend[0], res_bias=pend[1], bias=lw.b_qkv, q_out=r.q,
+                                      k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
+                cur = 1 - cur
+            self._attn(r, li)
+            ns = row_parallel(r.att, lw.w_o)
+            ops.skinny_addln_gemm(bufs[cur], lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps,
+                                  x_out=bufs[1 - cur], parts=parts, nsplit=ns, res_bias=lw.b_o, bias=lw.b_fc,
+                                  out=r.ff)
+            cur = 1 - cur
+            pend = (row_parallel(r.ff, lw.w_p), lw.b_p)
+        ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, parts=self.parts, nsplit=pend[0], bias=pend[1],
+                          out_bf16=self.h[:B])
+        self._lm_head_and_update(self.h[:B], B, penalty)
+
     def _decode_step(self, B: int, penalty: float):
+        if self._small_ok(B):
+            return self._decode_step_small(B, penalty)
         if self._overlap_ok(B):
             return self._decode_step_overlap(B, penalty)
         self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
@@ -575,7 +661,7 @@ class HipGPT2Engine:
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         f32, bf = torch.float32, torch.bfloat16
         x = ops.embed(tokens_d, pos_d, self.w.wte, self.w.wpe)
-        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl))
+        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl), self.prefill_split or 1)
         parts = torch.empty(nsplit, R, D, dtype=f32, device=dev)
         h = torch.empty(R, D, dtype=bf, device=dev)
         q = torch.empty(R, Dl, dtype=bf, device=dev)
@@ -613,7 +699,7 @@ class HipGPT2Engine:
         last = torch.tensor([sum(lens[: b + 1]) - 1 for b in range(len(prompts))], dtype=torch.int32, device=dev)
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         x = ops.embed(tokens, pos, self.w.wte, self.w.wpe)
-        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl))
+        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl), self.prefill_split or 1)
         parts = torch.empty(nsplit, R, D, device=dev)
         bf = torch.bfloat16
         h, q, att, ff = (torch.empty(R, n, dtype=bf, device=dev) for n in (D, Dl, Dl, Fl))

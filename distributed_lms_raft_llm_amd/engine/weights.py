@@ -54,6 +54,10 @@ class LayerWeights:
     s_qkv: torch.Tensor | None = None
     w_fc8: torch.Tensor | None = None
     s_fc: torch.Tensor | None = None
+    # MFMA-fragment-order copies (ops.shuffle_weight) of the LN-fed GEMMs for the latency path's
+    # skinny kernels; filled by the engine when that path is enabled
+    w_qkv_sh: torch.Tensor | None = None
+    w_fc_sh: torch.Tensor | None = None
 
 
 @dataclass

@@ -207,3 +207,41 @@ def reference_generate(
         hidden = model.forward(cur_tok[:, None], cur_pos[:, None], cache, rows)
         h_last = hidden[:, 0]
     return seqs
+
+
+@torch.no_grad()
+def teacher_forced_check(model: GPT2Reference, seq: list[int], prompt_len: int, repetition_penalty: float = 1.2,
+                         eps: float = 0.05) -> dict:
+    """Margin-aware exactness oracle for a generated sequence: run the fp32 reference once over
+    ``seq`` (teacher forcing), and at every generated position compare the produced token with the
+    reference's greedy choice under the repetition penalty of the prefix.  A position is
+    *decisive* when the reference's top-1 minus top-2 penalised logit exceeds ``eps``; at every
+    decisive position the token must be the reference's argmax.
+
+    Returns {"positions", "decisive", "mismatches": [(i, got, want, margin)], "min_margin"}."""
+    cfg = model.cfg
+    dev = model.device
+    S = len(seq)
+    if S <= prompt_len:
+        return {"positions": 0, "decisive": 0, "mismatches": [], "min_margin": float("inf")}
+    cache = KVCache.allocate(cfg, 1, S, dtype=model.dtype, device=dev)
+    toks = torch.tensor([seq], device=dev)
+    pos = torch.arange(S, device=dev)[None]
+    hidden = model.forward(toks, pos, cache, torch.zeros(1, dtype=torch.long, device=dev))[0]
+    logits = model.logits(hidden[prompt_len - 1: S - 1])  # row j predicts seq[prompt_len + j]
+    n = logits.shape[0]
+    seen = torch.zeros(n, cfg.vocab_size, dtype=torch.bool, device=dev)
+    for j in range(n):
+        seen[j, torch.tensor(seq[: prompt_len + j], device=dev)] = True
+    logits = apply_repetition_penalty(logits, seen, repetition_penalty)
+    top = logits.topk(2, dim=-1)
+    margin = (top.values[:, 0] - top.values[:, 1]).tolist()
+    want = top.indices[:, 0].tolist()
+    out = {"positions": n, "decisive": 0, "mismatches": [], "min_margin": min(margin)}
+    for j in range(n):
+        got = seq[prompt_len + j]
+        if margin[j] > eps:
+            out["decisive"] += 1
+            if got != want[j]:
+                out["mismatches"].append((prompt_len + j, got, want[j], margin[j]))
+    return out

@@ -27,11 +27,11 @@ LIB_DIR = _HERE / "_lib"
 LIB_PATH = LIB_DIR / "libdlms_hip.so"
 # debug variant: device-side range checks on every data-dependent index (common.h, DLMS_DEVICE_CHECKS)
 CHECKED_LIB_PATH = LIB_DIR / "libdlms_hip_checked.so"
-CHECK_UNITS = ("gemm", "attention", "decode", "encoder")
+CHECK_UNITS = ("gemm", "attention", "decode", "encoder", "skinny")
 CHECK_SITES = {1: "embed token id", 2: "position id", 3: "decode_update slot_map", 4: "decode_update token id",
                5: "decode_update sequence length", 6: "seen_set row", 7: "QKV scatter slot", 8: "QKV scatter position",
                9: "attention slot", 10: "BERT token id", 11: "seen_set token id"}
-SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip"]
+SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip", "skinny.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
 EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
@@ -128,6 +128,11 @@ def _bind(L):
         "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, I, I, P],
         "dlms_mean_pool": [P, P, P, P, I, I, P],
         "dlms_cosine": [P, P, P, I, I, I, F, P],
+        "dlms_skinny_gemm": [I, P, I, P, P, F, P, I, I, I, ctypes.POINTER(GemmEpi), P],
+        "dlms_attention_split": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, P],
+        "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
+                                   ctypes.POINTER(GemmEpi), P],
+        "dlms_skinny_addln_max_rows": [I],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -650,4 +655,237 @@ def cosine(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-8, out=None):
         out = torch.empty(a.shape[0], b.shape[0], dtype=torch.float32, device=a.device)
     _check(lib().dlms_cosine(_p(a), _p(b), _p(out), a.shape[0], b.shape[0], a.shape[1], float(eps), _stream()),
            "dlms_cosine")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Skinny (M <= 32) decode GEMMs on pre-shuffled weights + split-K flash-decode (skinny.hip)
+# ---------------------------------------------------------------------------------------------
+SKINNY_MAX_M = 32
+
+
+def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] bf16 (K contiguous) -> MFMA B-fragment order [N/16, K/32, 64, 8]: lane l of the
+    16x16x32 bf16 MFMA holds W[16 ng + (l & 15)][32 kb + 8 (l >> 4) + j] at [ng, kb, l, j], so one
+    contiguous KiB per (column group, k-block) is one wave-load straight into the B operand."""
+    if w.dim() != 2 or w.shape[0] % 16 or w.shape[1] % 32:
+        raise ValueError(f"shuffle_weight: need [N%16, K%32], got {tuple(w.shape)}")
+    N, K = w.shape
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(N // 16, K // 32, 64, 8).contiguous()
+
+
+def unshuffle_weight(ws: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``shuffle_weight`` (tests)."""
+    G, KB = ws.shape[0], ws.shape[1]
+    return ws.reshape(G, KB, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(G * 16, KB * 32)
+
+
+def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=None, out=None,
+                q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
+                argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0):
+    """Decode GEMM for M <= 32 rows against a ``shuffle_weight`` weight ([N/16, K/32, 64, 8]).
+
+    ``ln=(gamma, beta, eps)``: ``a`` is the f32 residual x [M, K] and the kernel LayerNorms it in
+    its prologue (EPI_BF16 / EPI_GELU_TANH / EPI_QKV); otherwise ``a`` is bf16 [M, K].
+    EPI_F32 adds ``acc + bias`` into ``out`` (f32 [M, N], in place: the residual stream);
+    EPI_PARTIAL stores the raw f32 partial (TP); EPI_ARGMAX writes one key per (row, 64 columns)
+    into ``argmax_out`` [M, >= N/64] exactly like ``gemm(..., EPI_ARGMAX)``."""
+    _req(w_sh, torch.bfloat16, "w_sh", 4)
+    G, KB = w_sh.shape[0], w_sh.shape[1]
+    if w_sh.shape[2] != 64 or w_sh.shape[3] != 8 or not w_sh.is_contiguous():
+        raise ValueError("skinny_gemm: w_sh must be a contiguous shuffle_weight() tensor")
+    N, K = G * 16, KB * 32
+    if ln is not None:
+        _req(a, torch.float32, "a", 2)
+        g_, b_, eps = ln
+        _req(g_, torch.float32, "ln gamma", 1)
+        _req(b_, torch.float32, "ln beta", 1)
+        if g_.numel() != K or b_.numel() != K or K > 2048 or K % 4:
+            raise ValueError("skinny_gemm: LN params must match K (<= 2048)")
+        if epi not in (EPI_BF16, EPI_GELU_TANH, EPI_QKV):
+            raise ValueError("skinny_gemm: the LayerNorm prologue feeds bf16 / GELU / QKV epilogues only")
+    else:
+        _req(a, torch.bfloat16, "a", 2)
+        if epi in (EPI_GELU_TANH, EPI_QKV):
+            raise ValueError("skinny_gemm: GELU / QKV epilogues take the LN prologue")
+        if a.stride(0) % 8 or a.data_ptr() % 16:
+            raise ValueError("skinny_gemm: bf16 A rows must be 16-byte aligned")
+    M = a.shape[0]
+    if a.shape[1] != K:
+        raise ValueError(f"skinny_gemm: a has K={a.shape[1]}, weight K={K}")
+    if M < 1 or M > SKINNY_MAX_M:
+        raise ValueError(f"skinny_gemm: 1 <= M <= {SKINNY_MAX_M}")
+    ep = GemmEpi()
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() < N:
+            raise ValueError("bias too short")
+        ep.bias = bias.data_ptr()
+    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_F32, EPI_PARTIAL):
+        want = torch.bfloat16 if epi in (EPI_BF16, EPI_GELU_TANH) else torch.float32
+        if out is None:
+            if epi == EPI_F32:
+                raise ValueError("skinny_gemm EPI_F32 accumulates into an existing out (the residual)")
+            out = torch.empty(M, N, dtype=want, device=a.device)
+        _req(out, want, "out", 2)
+        if out.shape[0] < M or out.shape[1] < N:
+            raise ValueError("out too small")
+        ep.out, ep.ldo = out.data_ptr(), out.stride(0)
+    elif epi == EPI_QKV:
+        for t, n in ((q_out, "q_out"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+            _req(t, torch.bfloat16, n)
+        _req(row_slot, torch.int32, "row_slot", 1)
+        _req(row_pos, torch.int32, "row_pos", 1)
+        if N % 3 or (N // 3) % 64:
+            raise ValueError("QKV N must be 3 * d_local (64-wide heads)")
+        d_local = N // 3
+        if k_cache.dim() != 4 or k_cache.shape != v_cache.shape or k_cache.shape[1] * 64 != d_local or \
+                k_cache.shape[3] != 64 or not k_cache.is_contiguous() or not v_cache.is_contiguous():
+            raise ValueError(f"cache shape {tuple(k_cache.shape)} incompatible with d_local={d_local}")
+        if q_out.shape[0] < M or q_out.shape[1] < d_local or row_slot.numel() < M or row_pos.numel() < M:
+            raise ValueError("qkv epilogue buffers too small")
+        ep.q_out, ep.ldq = q_out.data_ptr(), q_out.stride(0)
+        ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
+        ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
+        ep.n_heads, ep.t_max, ep.d_local, ep.n_slots = k_cache.shape[1], k_cache.shape[2], d_local, k_cache.shape[0]
+        out = q_out
+    elif epi == EPI_ARGMAX:
+        _req(argmax_out, torch.int64, "argmax_out", 2)
+        _req(seen, torch.int32, "seen", 2)
+        if N % 64 or argmax_out.shape[0] < M or argmax_out.shape[1] < N // 64 or seen.shape[0] < M or \
+                seen.shape[1] * 32 < vocab or col_offset % 64:
+            raise ValueError("argmax epilogue buffers too small / misaligned shard")
+        ep.argmax_out, ep.ldo, ep.seen = argmax_out.data_ptr(), argmax_out.stride(0), seen.data_ptr()
+        ep.seen_words, ep.vocab, ep.col_offset, ep.penalty = seen.stride(0), vocab, col_offset, penalty
+        out = argmax_out
+    else:
+        raise ValueError(f"skinny_gemm: unsupported epilogue {epi}")
+    lg, lb, le = (ln[0], ln[1], float(ln[2])) if ln is not None else (None, None, 0.0)
+    _check(lib().dlms_skinny_gemm(epi, _p(a), a.stride(0), _p(lg), _p(lb), le, _p(w_sh), M, N, K, ctypes.byref(ep),
+                                  _stream()), "dlms_skinny_gemm")
+    return out
+
+
+def skinny_addln_max_rows(K: int) -> int:
+    """Largest M the fused add+LN skinny GEMM takes at model width K (0 = unsupported)."""
+    return int(lib().dlms_skinny_addln_max_rows(int(K)))
+
+
+def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, beta, eps: float, *, x_out=None,
+                      parts=None, nsplit: int = 0, res_bias=None, bias=None, out=None, q_out=None, k_cache=None,
+                      v_cache=None, row_slot=None, row_pos=None):
+    """Fused residual update + LayerNorm + skinny GEMM (decode LN1 -> QKV, LN2 -> c_fc) for
+    M <= ``skinny_addln_max_rows(K)`` rows:
+
+        v = x_in + res_bias + sum(parts[:nsplit]);  x_out <- v (when given);
+        out = epi(bf16(LN(v)) @ W.T + bias)
+
+    ``x_out`` must not alias ``x_in`` (every workgroup re-reads x_in; one of them writes x_out):
+    the engine ping-pongs two residual buffers.  nsplit in {0, 1, 4}."""
+    _req(x_in, torch.float32, "x_in", 2)
+    _req(w_sh, torch.bfloat16, "w_sh", 4)
+    G, KB = w_sh.shape[0], w_sh.shape[1]
+    if w_sh.shape[2] != 64 or w_sh.shape[3] != 8 or not w_sh.is_contiguous():
+        raise ValueError("skinny_addln_gemm: w_sh must be a contiguous shuffle_weight() tensor")
+    N, K = G * 16, KB * 32
+    M = x_in.shape[0]
+    if x_in.shape[1] != K or M < 1 or M > skinny_addln_max_rows(K):
+        raise ValueError(f"skinny_addln_gemm: x_in {tuple(x_in.shape)} vs K={K}, max rows {skinny_addln_max_rows(K)}")
+    for t, n in ((gamma, "gamma"), (beta, "beta")):
+        _req(t, torch.float32, n, 1)
+        if t.numel() != K:
+            raise ValueError(f"{n} size")
+    if nsplit not in (0, 1, 4):
+        raise ValueError("skinny_addln_gemm: nsplit in {0, 1, 4}")
+    ldp, sstride = 0, 0
+    if nsplit:
+        _req(parts, torch.float32, "parts", 3)
+        if parts.shape[0] < nsplit or parts.shape[1] < M or parts.shape[2] < K or parts.stride(1) % 4 or \
+                parts.stride(0) % 4:
+            raise ValueError("skinny_addln_gemm: parts too small / misaligned")
+        ldp, sstride = parts.stride(1), parts.stride(0)
+    if res_bias is not None:
+        _req(res_bias, torch.float32, "res_bias", 1)
+        if res_bias.numel() != K:
+            raise ValueError("res_bias size")
+    if x_out is not None:
+        _req(x_out, torch.float32, "x_out", 2)
+        if x_out.shape[0] < M or x_out.shape[1] < K or x_out.stride(0) != x_in.stride(0):
+            raise ValueError("skinny_addln_gemm: x_out must match x_in's layout")
+        if x_out.data_ptr() == x_in.data_ptr():
+            raise ValueError("skinny_addln_gemm: x_out must not alias x_in (ping-pong the residual)")
+    if x_in.stride(0) % 4 or x_in.data_ptr() % 16:
+        raise ValueError("skinny_addln_gemm: x rows must be 16-byte aligned")
+    ep = GemmEpi()
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() < N:
+            raise ValueError("bias too short")
+        ep.bias = bias.data_ptr()
+    if epi == EPI_GELU_TANH:
+        if out is None:
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=x_in.device)
+        _req(out, torch.bfloat16, "out", 2)
+        if out.shape[0] < M or out.shape[1] < N:
+            raise ValueError("out too small")
+        ep.out, ep.ldo = out.data_ptr(), out.stride(0)
+    elif epi == EPI_QKV:
+        for t, n in ((q_out, "q_out"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+            _req(t, torch.bfloat16, n)
+        _req(row_slot, torch.int32, "row_slot", 1)
+        _req(row_pos, torch.int32, "row_pos", 1)
+        if N % 3 or (N // 3) % 64:
+            raise ValueError("QKV N must be 3 * d_local (64-wide heads)")
+        d_local = N // 3
+        if k_cache.dim() != 4 or k_cache.shape != v_cache.shape or k_cache.shape[1] * 64 != d_local or \
+                k_cache.shape[3] != 64 or not k_cache.is_contiguous() or not v_cache.is_contiguous():
+            raise ValueError(f"cache shape {tuple(k_cache.shape)} incompatible with d_local={d_local}")
+        if q_out.shape[0] < M or q_out.shape[1] < d_local or row_slot.numel() < M or row_pos.numel() < M:
+            raise ValueError("qkv epilogue buffers too small")
+        ep.q_out, ep.ldq = q_out.data_ptr(), q_out.stride(0)
+        ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
+        ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
+        ep.n_heads, ep.t_max, ep.d_local, ep.n_slots = k_cache.shape[1], k_cache.shape[2], d_local, k_cache.shape[0]
+        out = q_out
+    else:
+        raise ValueError("skinny_addln_gemm: QKV or GELU epilogue")
+    _check(lib().dlms_skinny_addln_gemm(epi, _p(x_in), _p(x_out), x_in.stride(0), _p(parts) if nsplit else None, ldp,
+                                        sstride, nsplit, _p(res_bias), _p(gamma), _p(beta), float(eps), _p(w_sh), M, N,
+                                        K, ctypes.byref(ep), _stream()), "dlms_skinny_addln_gemm")
+    return out
+
+
+def attention_split_waves(kv_len_max: int) -> int:
+    """Waves per (row, head) for ``attention_split``: about 32 keys per wave, 2..16."""
+    for nw in (2, 4, 8, 16):
+        if kv_len_max <= 32 * nw:
+            return nw
+    return 16
+
+
+def attention_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
+                    row_kvlen: torch.Tensor, out: torch.Tensor | None = None, scale: float | None = None,
+                    waves: int = 16):
+    """Split-K flash-decode: one workgroup of ``waves`` waves per (row, head), each streaming a
+    slice of the keys, merged by log-sum-exp.  Same contract as ``row_attention``."""
+    _req(q, torch.bfloat16, "q", 2)
+    _req(k_cache, torch.bfloat16, "k_cache", 4)
+    _req(v_cache, torch.bfloat16, "v_cache", 4)
+    _req(row_slot, torch.int32, "row_slot", 1)
+    _req(row_kvlen, torch.int32, "row_kvlen", 1)
+    R = q.shape[0]
+    S, H, T, hd = k_cache.shape
+    if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64:
+        raise ValueError("attention_split: bad shapes")
+    if row_slot.numel() < R or row_kvlen.numel() < R:
+        raise ValueError("attention_split: index arrays too short")
+    if waves not in (2, 4, 8, 16):
+        raise ValueError("attention_split: waves in {2, 4, 8, 16}")
+    if out is None:
+        out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=q.device)
+    _req(out, torch.bfloat16, "out", 2)
+    sc = (1.0 / 8.0) if scale is None else scale
+    _check(lib().dlms_attention_split(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
+                                      _p(out), out.stride(0), R, H, T, S, float(sc), int(waves), _stream()),
+           "attention_split")
     return out

@@ -27,10 +27,18 @@ __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ toke
 // max over a row's partial argmax keys, one wave per row (keys(b, p) = keys[b * sb + p * sp])
 __device__ __forceinline__ unsigned long long wave_key_max(const unsigned long long* __restrict__ keys, int b,
                                                            int nparts, long long sb, long long sp, int lane) {
+    // 8 independent loads in flight per lane per round (the LM head leaves ~800 partial keys per
+    // row at TP=1: a one-load-at-a-time loop paid ~13 dependent round trips per decode step)
     unsigned long long best = 0ull;
-    for (int p = lane; p < nparts; p += 64) {
-        const unsigned long long k = keys[(size_t)b * sb + (size_t)p * sp];
-        best = k > best ? k : best;
+    for (int p0 = 0; p0 < nparts; p0 += 64 * 8) {
+        unsigned long long k[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 + lane + 64 * u;
+            k[u] = p < nparts ? keys[(size_t)b * sb + (size_t)p * sp] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) best = k[u] > best ? k[u] : best;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

@@ -1,0 +1,681 @@
+// Skinny (decode, M <= 32 rows) MFMA GEMMs and split-K flash-decode attention: the latency path.
+//
+// At batch 1-32 a decode step is a chain of ~60 weight-streaming kernels whose runtime is launch +
+// memory latency, not FLOPs (a 64x64-tile GEMM puts only N/64 = 36 workgroups on the 256 CUs for
+// GPT-2's QKV).  These kernels are shaped for that regime:
+//
+//  * weights are PRE-SHUFFLED once at load time into MFMA B-fragment order
+//    (engine/weights.py: [N/16][K/32][64 lanes][8 bf16]), so every wave-instruction loads one
+//    contiguous KiB straight into the B operand of v_mfma_f32_16x16x32_bf16 -- no LDS round trip for
+//    the streamed operand, perfectly coalesced, and one 16-column group per wave keeps N/16
+//    groups x (K split over the workgroup's waves) wave-loads in flight;
+//  * the (tiny) activation is the A operand: either x (f32 residual) normalised by a fused
+//    LayerNorm prologue into an LDS bf16 image (LN1 -> QKV, LN2 -> c_fc: no separate LN kernel),
+//    or a bf16 activation read as A fragments straight from L2 (att -> out-proj, ff -> c_proj);
+//  * K is split over the waves of a workgroup and the partial accumulators are summed in a fixed
+//    order through LDS (deterministic), so one workgroup owns whole output columns: the row-parallel
+//    projections add bias + residual in place (x += ...) with no split-K slabs and no add+LN pass.
+//
+// Epilogues: EPI_BF16 / EPI_GELU_TANH / EPI_QKV (q out + K/V scattered into the cache) /
+// EPI_F32 (x += acc + bias, in place) / EPI_PARTIAL (TP: raw partial for the all-reduce) /
+// EPI_ARGMAX (repetition penalty + per-row argmax key per 64 columns, the LM-head layout of gemm.hip).
+#include "common.h"
+
+enum { SK_BF16 = 0, SK_GELU_TANH = 1, SK_F32 = 3, SK_QKV = 4, SK_ARGMAX = 5, SK_PARTIAL = 6 };
+
+#define SK_MAX_LN_V4 8  // LN prologue: K <= 64 lanes * 4 * 8 = 2048
+
+// Weight-fragment loads: plain (default-policy) loads keep the streamed weights eligible for the
+// 256 MiB Infinity Cache, which holds most of GPT-2-small's 248 MB per-step weight stream at batch
+// 1; DLMS_SKINNY_NT=1 builds non-temporal loads instead (cdna guide: nt-weights row).
+#ifndef DLMS_SKINNY_NT
+#define DLMS_SKINNY_NT 0
+#endif
+__device__ __forceinline__ bf16x8_t load_wfrag(const bf16x8_t* p) {
+#if DLMS_SKINNY_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
+// A fragment of rows [16 mt, 16 mt + 16) at k-block kb from the LDS LayerNorm image
+__device__ __forceinline__ bf16x8_t lds_a_frag(const char* img, int row_bytes, int row, int kb, int g) {
+    return *reinterpret_cast<const bf16x8_t*>(img + row * row_bytes + (kb * 32 + g * 8) * 2);
+}
+
+// LayerNorm of rows [0, M) of x (f32, ldx) into an LDS bf16 image of 16*MT rows (rows >= M zero).
+// Wave w normalises rows w, w + NW, ...; two-pass statistics in fp32 like norm.hip.
+template <int NW, int MT>
+__device__ __forceinline__ void ln_prologue(const float* __restrict__ x, int ldx, const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, int M, int K, float eps, char* img,
+                                            int row_bytes) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int nv = K >> 2;
+    for (int r = wave; r < 16 * MT; r += NW) {
+        char* dst = img + r * row_bytes;
+        if (r >= M) {
+            for (int c = lane; c < nv; c += 64) *reinterpret_cast<uint2*>(dst + c * 8) = make_uint2(0u, 0u);
+            continue;
+        }
+        const float4* xr = reinterpret_cast<const float4*>(x + (size_t)r * ldx);
+        float4 v[SK_MAX_LN_V4];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < SK_MAX_LN_V4; ++i) {
+            const int c = lane + 64 * i;
+            v[i] = c < nv ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        }
+        const float mean = wave_sum(s) / (float)K;
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < SK_MAX_LN_V4; ++i) {
+            const int c = lane + 64 * i;
+            if (c < nv) {
+                const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+                ss += (a * a + b * b) + (cc * cc + d * d);
+            }
+        }
+        const float rstd = rsqrtf(wave_sum(ss) / (float)K + eps);
+        const float4* g4 = reinterpret_cast<const float4*>(gamma);
+        const float4* b4 = reinterpret_cast<const float4*>(beta);
+#pragma unroll
+        for (int i = 0; i < SK_MAX_LN_V4; ++i) {
+            const int c = lane + 64 * i;
+            if (c < nv) {
+                const float4 gg = g4[c], bb = b4[c];
+                uint2 p;
+                p.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+                p.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+                *reinterpret_cast<uint2*>(dst + c * 8) = p;
+            }
+        }
+    }
+}
+
+// Column-owning epilogue of one wave: accumulator element r of row tile t is (row 16t + 4g + r, col).
+template <int EPI, int MT>
+__device__ __forceinline__ void skinny_store(const f32x4_t* acc, int M, int col, int g, const GemmEpi& ep) {
+    const float bv = (EPI != SK_PARTIAL && ep.bias) ? ep.bias[col] : 0.f;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * t + g * 4 + r;
+            if (row >= M) continue;
+            float v = acc[t][r] + bv;
+            if constexpr (EPI == SK_BF16) {
+                reinterpret_cast<bf16_t*>(ep.out)[(size_t)row * ep.ldo + col] = f32_to_bf16(v);
+            } else if constexpr (EPI == SK_GELU_TANH) {
+                reinterpret_cast<bf16_t*>(ep.out)[(size_t)row * ep.ldo + col] = f32_to_bf16(gelu_tanh(v));
+            } else if constexpr (EPI == SK_F32) {
+                float* o = reinterpret_cast<float*>(ep.out) + (size_t)row * ep.ldo + col;
+                *o = *o + v;  // residual stream, updated in place (x is not an operand of this GEMM)
+            } else if constexpr (EPI == SK_PARTIAL) {
+                reinterpret_cast<float*>(ep.out)[(size_t)row * ep.ldo + col] = acc[t][r];
+            } else if constexpr (EPI == SK_QKV) {
+                const int part = col / ep.d_local;
+                const int within = col - part * ep.d_local;
+                const bf16_t hv = f32_to_bf16(v);
+                if (part == 0) {
+                    ep.q_out[(size_t)row * ep.ldq + within] = hv;
+                } else {
+                    const int head = within >> 6, dim = within & 63;
+                    const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
+                    const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
+                    (part == 1 ? ep.k_cache : ep.v_cache)[((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim] = hv;
+                }
+            }
+        }
+}
+
+// grid.x = column-group blocks of CG groups (16 columns each); block = 64*NW threads.
+// Waves per column group WPG = NW / CG split the K/32 k-blocks evenly (fixed-order LDS reduction);
+// each wave holds at most KBW k-blocks and issues ALL its B (and, without the LN prologue, A)
+// fragment loads before the first MFMA -- the latency-bound regime wants every byte in flight.
+template <int EPI, bool LN, int MT, int NW, int CG, int KBW>
+__global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const void* __restrict__ A, int lda,
+                                                            const float* __restrict__ ln_g, const float* __restrict__ ln_b,
+                                                            float eps, const bf16_t* __restrict__ Wsh, int M, int N,
+                                                            int K, GemmEpi ep) {
+    constexpr int WPG = NW / CG;
+    static_assert(NW % CG == 0, "whole waves per column group");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int cgi = wave / WPG;       // column group within the block
+    const int kpart = wave % WPG;     // K slice of this wave
+    const int ng = blockIdx.x * CG + cgi;
+    const int nkb = K >> 5;
+    const int per = (nkb + WPG - 1) / WPG;
+    const int kb0 = kpart * per < nkb ? kpart * per : nkb;
+    const int nk = (kb0 + per < nkb ? kb0 + per : nkb) - kb0;  // k-blocks of this wave (<= KBW)
+    const int g = lane >> 4, fr = lane & 15;
+    const int row_bytes = K * 2 + 16;  // padded LN image rows: conflict-free ds_read_b128 fragments
+
+    const int kbl = nk > 0 ? kb0 : 0;  // a wave with no k-blocks still loads (and ignores) block 0
+    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wsh) + ((size_t)ng * nkb + kbl) * 64 + lane;
+    const int last = nk > 0 ? nk - 1 : 0;
+    bf16x8_t b[KBW];
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
+    bf16x8_t a[LN ? 1 : KBW][MT];
+    if constexpr (!LN) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            int row = 16 * t + fr;
+            row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
+            const bf16_t* ar = reinterpret_cast<const bf16_t*>(A) + (size_t)row * lda + kbl * 32 + g * 8;
+#pragma unroll
+            for (int u = 0; u < KBW; ++u) a[u][t] = *reinterpret_cast<const bf16x8_t*>(ar + (u < nk ? u : last) * 32);
+        }
+    }
+
+    f32x4_t acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+    if constexpr (LN) {
+        ln_prologue<NW, MT>(reinterpret_cast<const float*>(A), lda, ln_g, ln_b, M, K, eps, smem, row_bytes);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            if (u >= nk) continue;  // wave-uniform; constant register indices keep b[]/a[] in VGPRs
+            bf16x8_t av;
+            if constexpr (LN)
+                av = lds_a_frag(smem, row_bytes, 16 * t + fr, kb0 + u, g);
+            else
+                av = a[u][t];
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b[u], acc[t], 0, 0, 0);
+        }
+    }
+
+    // ---- fixed-order reduction of the WPG K slices of each column group ----
+    float* red = reinterpret_cast<float*>(smem);
+    if constexpr (WPG > 1) {
+        __syncthreads();  // LN image no longer read
+        if (kpart > 0) {
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                *reinterpret_cast<f32x4_t*>(red + ((size_t)(wave * MT + t) * 64 + lane) * 4) = acc[t];
+        }
+        __syncthreads();
+        if (kpart == 0) {
+#pragma unroll
+            for (int s = 1; s < WPG; ++s)
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    const f32x4_t o = *reinterpret_cast<const f32x4_t*>(red + ((size_t)((wave + s) * MT + t) * 64 + lane) * 4);
+                    acc[t] += o;
+                }
+        }
+    }
+
+    const int col = ng * 16 + fr;
+    if constexpr (EPI == SK_ARGMAX) {
+        // penalty + argmax over this block's CG*16 columns -> one key per (row, 64-column group)
+        static_assert(CG * 16 == 64, "argmax epilogue: one 64-column key group per block");
+        __shared__ unsigned long long kred[CG][32];
+        if (kpart == 0) {
+            const int gcol = col + ep.col_offset;
+            const bool valid = gcol < ep.vocab;
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * t + g * 4 + r;
+                    const int srow = row < M ? row : M - 1;
+                    float v = acc[t][r];
+                    const unsigned int bits = ep.seen[(size_t)srow * ep.seen_words + (gcol >> 5)];
+                    if ((bits >> (gcol & 31)) & 1u) v = v < 0.f ? v * ep.penalty : v / ep.penalty;
+                    unsigned long long key =
+                        valid ? (((unsigned long long)f32_ordered(v) << 32) | (unsigned long long)(~(unsigned int)gcol)) : 0ull;
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) {
+                        const unsigned long long other = __shfl_xor(key, o, 64);
+                        key = other > key ? other : key;
+                    }
+                    if (fr == 0) kred[cgi][row] = key;
+                }
+        }
+        __syncthreads();
+        for (int row = threadIdx.x; row < M && row < 16 * MT; row += 64 * NW) {
+            unsigned long long b = kred[0][row];
+#pragma unroll
+            for (int c = 1; c < CG; ++c) b = kred[c][row] > b ? kred[c][row] : b;
+            ep.argmax_out[(size_t)row * ep.ldo + blockIdx.x] = b;
+        }
+        return;
+    }
+    if (kpart != 0) return;
+    skinny_store<EPI, MT>(acc, M, col, g, ep);
+}
+
+template <int EPI, bool LN, int MT, int NW, int CG, int KBW>
+static hipError_t launch_skinny(const void* A, int lda, const float* g, const float* b, float eps, const bf16_t* W,
+                                int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
+    size_t lds = 0;
+    if (LN) lds = (size_t)16 * MT * (K * 2 + 16);
+    const size_t red = (size_t)NW * MT * 64 * 4 * sizeof(float);
+    if (NW / CG > 1 && red > lds) lds = red;
+    static bool attr_set = false;
+    if (!attr_set && lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<EPI, LN, MT, NW, CG, KBW>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((skinny_gemm_kernel<EPI, LN, MT, NW, CG, KBW>), dim3(N / (16 * CG)), dim3(64 * NW), lds, stream,
+                       A, lda, g, b, eps, W, M, N, K, ep);
+    return hipGetLastError();
+}
+
+// k-blocks per wave -> the smallest register budget KBW that holds them
+template <int EPI, bool LN, int MT, int NW, int CG>
+static hipError_t skinny_kbw(const void* A, int lda, const float* g, const float* b, float eps, const bf16_t* W,
+                             int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
+    const int per = ((K >> 5) + NW / CG - 1) / (NW / CG);
+    if (per <= 4) return launch_skinny<EPI, LN, MT, NW, CG, 4>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    if (per <= 8) return launch_skinny<EPI, LN, MT, NW, CG, 8>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    if (per <= 12) return launch_skinny<EPI, LN, MT, NW, CG, 12>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    if (per <= 16) return launch_skinny<EPI, LN, MT, NW, CG, 16>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    return hipErrorInvalidValue;
+}
+
+// Geometry per epilogue family (waves split K; one 16-column group per wave group):
+//   LN-fed column-parallel GEMMs (QKV, c_fc): 4 waves per group;
+//   row-parallel projections (N = d: few column groups): out-proj 8 waves, c_proj (K = 4d) 16;
+//   LM head: 4 column groups of 4 waves (64 columns -> one argmax key per row and block).
+template <int EPI, bool LN, int MT>
+static hipError_t skinny_dispatch(const void* A, int lda, const float* g, const float* b, float eps, const bf16_t* W,
+                                  int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
+    if constexpr (EPI == SK_ARGMAX) {
+        return skinny_kbw<EPI, LN, MT, 16, 4>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    } else if constexpr (EPI == SK_F32 || EPI == SK_PARTIAL) {
+        if (K > 2048) return skinny_kbw<EPI, LN, MT, 16, 1>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+        return skinny_kbw<EPI, LN, MT, 8, 1>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    } else {
+        return skinny_kbw<EPI, LN, MT, 4, 1>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    }
+}
+
+template <int EPI, bool LN>
+static hipError_t skinny_mt(const void* A, int lda, const float* g, const float* b, float eps, const bf16_t* W, int M,
+                            int N, int K, const GemmEpi& ep, hipStream_t stream) {
+    if (M <= 16) return skinny_dispatch<EPI, LN, 1>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+    return skinny_dispatch<EPI, LN, 2>(A, lda, g, b, eps, W, M, N, K, ep, stream);
+}
+
+// A: f32 x [M][lda] when ln_g != nullptr (fused LayerNorm prologue), else bf16 [M][lda].
+// Wsh: pre-shuffled [N/16][K/32][64][8] bf16.
+extern "C" hipError_t dlms_skinny_gemm(int epi, const void* A, int lda, const float* ln_g, const float* ln_b, float eps,
+                                       const void* Wsh, int M, int N, int K, const GemmEpi* ep, hipStream_t stream) {
+    if (M <= 0 || M > 32 || N % 16 || K % 32 || K <= 0) return hipErrorInvalidValue;
+    const bool ln = ln_g != nullptr;
+    if (ln && (K % 4 || K > 64 * 4 * SK_MAX_LN_V4)) return hipErrorInvalidValue;
+    if (epi == SK_ARGMAX && N % 64) return hipErrorInvalidValue;
+    const bf16_t* W = reinterpret_cast<const bf16_t*>(Wsh);
+#define SK_LN(E) \
+    case E:       \
+        return ln ? skinny_mt<E, true>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream) : hipErrorInvalidValue;
+#define SK_NOLN(E) \
+    case E:         \
+        return ln ? hipErrorInvalidValue : skinny_mt<E, false>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream);
+    switch (epi) {
+        case SK_BF16:
+            return ln ? skinny_mt<SK_BF16, true>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream)
+                      : skinny_mt<SK_BF16, false>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream);
+        SK_LN(SK_GELU_TANH)
+        SK_LN(SK_QKV)
+        SK_NOLN(SK_F32)
+        SK_NOLN(SK_ARGMAX)
+        SK_NOLN(SK_PARTIAL)
+        default: return hipErrorInvalidValue;
+    }
+#undef SK_LN
+#undef SK_NOLN
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused residual update + LayerNorm + skinny GEMM: the decode path's LN1 -> QKV and LN2 -> c_fc at
+// M <= 4 * RPW rows (one 16-row MFMA tile; rows >= M are never stored).
+//
+//   v = x_in + res_bias + sum_{s < NSPLIT} parts[s]        (the pending row-parallel update:
+//                                                           split-K slabs, or the TP all-reduce)
+//   block 0 writes x_out = v  -- the residual stream moves to the OTHER ping-pong buffer, so no
+//                                block ever reads a row another block has already advanced;
+//   A = bf16(LN(v) * gamma + beta) -> LDS -> v_mfma_f32_16x16x32_bf16 against pre-shuffled W.
+//
+// Load order: all weight fragments of the wave first (HBM), then the activation rows (L2), so
+// both are in flight together -- one memory round trip before the LayerNorm, not two.
+template <int EPI, int NSPLIT, int NV4, int RPW, int KBW>
+__global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restrict__ x_in, float* __restrict__ x_out,
+                                                         int ldx, const float* __restrict__ parts, int ldp,
+                                                         long long split_stride, const float* __restrict__ res_bias,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         float eps, const bf16_t* __restrict__ Wsh, int M, int N, int K,
+                                                         GemmEpi ep) {
+    constexpr int NW = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int ng = blockIdx.x;
+    const int nkb = K >> 5;
+    const int per = (nkb + NW - 1) / NW;
+    const int kb0 = wave * per < nkb ? wave * per : nkb;
+    const int nk = (kb0 + per < nkb ? kb0 + per : nkb) - kb0;
+    const int kbl = nk > 0 ? kb0 : 0;
+    const int last = nk > 0 ? nk - 1 : 0;
+    const int g = lane >> 4, fr = lane & 15;
+    const int row_bytes = K * 2 + 16;
+    const int nv = K >> 2;
+
+    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wsh) + ((size_t)ng * nkb + kbl) * 64 + lane;
+    bf16x8_t b[KBW];
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
+
+    int cidx[NV4];
+    bool valid[NV4];
+#pragma unroll
+    for (int i = 0; i < NV4; ++i) {
+        const int c = lane + 64 * i;
+        valid[i] = c < nv;
+        cidx[i] = valid[i] ? c : nv - 1;
+    }
+    float4 v[RPW][NV4];
+    float4 pv[RPW][NSPLIT > 0 ? NSPLIT : 1][NV4];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        int row = wave + NW * i;
+        row = row < M ? row : M - 1;
+        const float4* xr = reinterpret_cast<const float4*>(x_in + (size_t)row * ldx);
+#pragma unroll
+        for (int c = 0; c < NV4; ++c) v[i][c] = xr[cidx[c]];
+#pragma unroll
+        for (int s = 0; s < NSPLIT; ++s) {
+            const float4* pr = reinterpret_cast<const float4*>(parts + (size_t)s * split_stride + (size_t)row * ldp);
+#pragma unroll
+            for (int c = 0; c < NV4; ++c) pv[i][s][c] = pr[cidx[c]];
+        }
+    }
+    float4 gv[NV4], bv[NV4], rb[NV4];
+#pragma unroll
+    for (int c = 0; c < NV4; ++c) {
+        gv[c] = reinterpret_cast<const float4*>(gamma)[cidx[c]];
+        bv[c] = reinterpret_cast<const float4*>(beta)[cidx[c]];
+        rb[c] = res_bias ? reinterpret_cast<const float4*>(res_bias)[cidx[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const int row = wave + NW * i;
+        if (row >= M) continue;  // wave-uniform
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NV4; ++c) {
+            float4 t = v[i][c];
+            t.x += rb[c].x; t.y += rb[c].y; t.z += rb[c].z; t.w += rb[c].w;
+#pragma unroll
+            for (int sp = 0; sp < NSPLIT; ++sp) {
+                t.x += pv[i][sp][c].x; t.y += pv[i][sp][c].y; t.z += pv[i][sp][c].z; t.w += pv[i][sp][c].w;
+            }
+            if (!valid[c]) t = make_float4(0.f, 0.f, 0.f, 0.f);
+            v[i][c] = t;
+            s += (t.x + t.y) + (t.z + t.w);
+        }
+        if (x_out != nullptr && blockIdx.x == 0) {
+#pragma unroll
+            for (int c = 0; c < NV4; ++c)
+                if (valid[c]) reinterpret_cast<float4*>(x_out + (size_t)row * ldx)[cidx[c]] = v[i][c];
+        }
+        const float mean = wave_sum(s) / (float)K;
+        float ss = 0.f;
+#pragma unroll
+        for (int c = 0; c < NV4; ++c) {
+            if (valid[c]) {
+                const float a0 = v[i][c].x - mean, a1 = v[i][c].y - mean, a2 = v[i][c].z - mean, a3 = v[i][c].w - mean;
+                ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+            }
+        }
+        const float rstd = rsqrtf(wave_sum(ss) / (float)K + eps);
+        char* dst = smem + row * row_bytes;
+#pragma unroll
+        for (int c = 0; c < NV4; ++c) {
+            if (valid[c]) {
+                const float4 t = v[i][c];
+                uint2 p;
+                p.x = pack_bf16x2((t.x - mean) * rstd * gv[c].x + bv[c].x, (t.y - mean) * rstd * gv[c].y + bv[c].y);
+                p.y = pack_bf16x2((t.z - mean) * rstd * gv[c].z + bv[c].z, (t.w - mean) * rstd * gv[c].w + bv[c].w);
+                *reinterpret_cast<uint2*>(dst + cidx[c] * 8) = p;
+            }
+        }
+    }
+    __syncthreads();
+
+    f32x4_t acc[1] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) {
+        if (u >= nk) continue;
+        const bf16x8_t av = lds_a_frag(smem, row_bytes, fr, kb0 + u, g);  // rows >= M: never stored
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b[u], acc[0], 0, 0, 0);
+    }
+    __syncthreads();  // LN image no longer read: reuse it for the K-slice reduction
+    float* red = reinterpret_cast<float*>(smem);
+    if (wave > 0) *reinterpret_cast<f32x4_t*>(red + ((size_t)wave * 64 + lane) * 4) = acc[0];
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int s = 1; s < NW; ++s) acc[0] += *reinterpret_cast<const f32x4_t*>(red + ((size_t)s * 64 + lane) * 4);
+    skinny_store<EPI, 1>(acc, M, ng * 16 + fr, g, ep);
+}
+
+template <int EPI, int NSPLIT, int NV4, int RPW>
+static hipError_t launch_addln(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
+                               const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M,
+                               int N, int K, const GemmEpi& ep, hipStream_t stream) {
+    constexpr int KBW = NV4 <= 2 ? 4 : (NV4 <= 4 ? 8 : (NV4 == 5 ? 12 : 16));  // >= K/32/4 for K <= 256 * NV4
+    const size_t lds = (size_t)16 * (K * 2 + 16);
+    hipLaunchKernelGGL((skinny_addln_kernel<EPI, NSPLIT, NV4, RPW, KBW>), dim3(N / 16), dim3(256), lds, stream, x_in,
+                       x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep);
+    return hipGetLastError();
+}
+
+template <int EPI, int NSPLIT, int NV4>
+static hipError_t addln_rpw(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
+                            const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M, int N,
+                            int K, const GemmEpi& ep, hipStream_t stream) {
+    if (M <= 4) return launch_addln<EPI, NSPLIT, NV4, 1>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+    if constexpr (NV4 <= 4) {
+        if (M <= 8) return launch_addln<EPI, NSPLIT, NV4, 2>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int EPI, int NSPLIT>
+static hipError_t addln_nv4(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
+                            const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M, int N,
+                            int K, const GemmEpi& ep, hipStream_t stream) {
+    switch ((K / 4 + 63) / 64) {
+        case 1: return addln_rpw<EPI, NSPLIT, 1>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        case 2: return addln_rpw<EPI, NSPLIT, 2>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        case 3: return addln_rpw<EPI, NSPLIT, 3>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        case 4: return addln_rpw<EPI, NSPLIT, 4>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        case 5: return addln_rpw<EPI, NSPLIT, 5>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        case 7: return addln_rpw<EPI, NSPLIT, 7>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// Max rows of the fused add+LN skinny GEMM for a model width K (0: not supported).
+extern "C" int dlms_skinny_addln_max_rows(int K) {
+    const int nv4 = (K / 4 + 63) / 64;
+    if (K % 32 || K <= 0 || nv4 == 6 || nv4 > 7) return 0;
+    return nv4 <= 4 ? 8 : 4;
+}
+
+extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const float* x_in, float* x_out, int ldx, const float* parts,
+                                             int ldp, long long split_stride, int nsplit, const float* res_bias,
+                                             const float* gamma, const float* beta, float eps, const void* Wsh, int M,
+                                             int N, int K, const GemmEpi* ep, hipStream_t stream) {
+    if (M <= 0 || M > dlms_skinny_addln_max_rows(K) || N % 16) return hipErrorInvalidValue;
+    const bf16_t* W = reinterpret_cast<const bf16_t*>(Wsh);
+#define ADDLN(E, NS) \
+    return addln_nv4<E, NS>(x_in, x_out, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, W, M, N, K, *ep, stream)
+#define ADDLN_EPI(E)                    \
+    switch (nsplit) {                   \
+        case 0: ADDLN(E, 0);            \
+        case 1: ADDLN(E, 1);            \
+        case 4: ADDLN(E, 4);            \
+        default: return hipErrorInvalidValue; \
+    }
+    switch (epi) {
+        case SK_QKV: ADDLN_EPI(SK_QKV)
+        case SK_GELU_TANH: ADDLN_EPI(SK_GELU_TANH)
+        default: return hipErrorInvalidValue;
+    }
+#undef ADDLN_EPI
+#undef ADDLN
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-K flash-decode (K5): ONE WORKGROUP per (row, head), NW waves each streaming a contiguous
+// slice of the row's keys with the online softmax of attn_wave_kernel (lane (g = lane>>3, c =
+// lane&7) owns dims [8c, 8c+8) of keys 8i + g), then a log-sum-exp merge of the NW partial
+// (max, sum, acc[64]) triples in a fixed order through LDS.  At batch 1 and 1024 cached keys this
+// puts 12 x NW waves on the KV stream instead of 12.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                           const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                                           const int* __restrict__ row_slot,
+                                                           const int* __restrict__ row_kvlen, bf16_t* out, int ldo,
+                                                           int H, int t_max, int n_slots, float scale_log2) {
+    __shared__ float part[NW][8][10];  // per wave, per dim chunk c: m, l, acc[8]
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = blockIdx.x;
+    const int r = blockIdx.y;
+    const int g = lane >> 3;
+    const int c = lane & 7;
+    const int slot = (int)dlms_idx(row_slot[r], n_slots, CHK_ATTN_SLOT);
+    int kvlen = row_kvlen[r];
+    kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
+    const int span = ((kvlen + NW - 1) / NW + 7) & ~7;
+    const int t_lo = wave * span;
+    const int t_hi = t_lo + span < kvlen ? t_lo + span : kvlen;
+    const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+    const bf16_t* K = kc + head_off + c * 8;
+    const bf16_t* V = vc + head_off + c * 8;
+
+    float qf[8];
+    unpack8(*reinterpret_cast<const uint4*>(q + (size_t)r * ldq + h * 64 + c * 8), qf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[j] *= scale_log2;
+
+    float m = -INFINITY, l = 0.f;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 4;
+    for (int t0 = t_lo; t0 < t_hi; t0 += 8 * U) {
+        uint4 kr[U], vr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int t = t0 + u * 8 + g;
+            t = t < t_hi ? t : t_hi - 1;
+            typedef unsigned int u32x4n_t __attribute__((ext_vector_type(4)));
+            const u32x4n_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4n_t*>(K + (size_t)t * 64));
+            const u32x4n_t b = __builtin_nontemporal_load(reinterpret_cast<const u32x4n_t*>(V + (size_t)t * 64));
+            kr[u] = make_uint4(a.x, a.y, a.z, a.w);
+            vr[u] = make_uint4(b.x, b.y, b.z, b.w);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float kf[8];
+            unpack8(kr[u], kf);
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
+            s += __shfl_xor(s, 1, 64);
+            s += __shfl_xor(s, 2, 64);
+            s += __shfl_xor(s, 4, 64);
+            if (t0 + u * 8 + g < t_hi) {
+                const float m_new = fmaxf(m, s);
+                const float corr = exp2f(m - m_new);
+                const float p = exp2f(s - m_new);
+                float vf[8];
+                unpack8(vr[u], vf);
+                l = l * corr + p;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] = acc[j] * corr + p * vf[j];
+                m = m_new;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+        const float m_o = __shfl_xor(m, o, 64);
+        const float l_o = __shfl_xor(l, o, 64);
+        const float m_n = fmaxf(m, m_o);
+        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
+        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
+        l = l * a + l_o * b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x_o = __shfl_xor(acc[j], o, 64);
+            acc[j] = acc[j] * a + x_o * b;
+        }
+        m = m_n;
+    }
+    if (g == 0) {
+        part[wave][c][0] = m;
+        part[wave][c][1] = l;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part[wave][c][2 + j] = acc[j];
+    }
+    __syncthreads();
+    if (wave == 0 && g == 0) {
+        float M_ = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) M_ = fmaxf(M_, part[w][c][0]);
+        float L = 0.f, o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const float mw = part[w][c][0];
+            if (mw == -INFINITY) continue;  // empty slice
+            const float f = exp2f(mw - M_);
+            L += part[w][c][1] * f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o8[j] += part[w][c][2 + j] * f;
+        }
+        const float inv = 1.f / L;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o8[j] *= inv;
+        *reinterpret_cast<uint4*>(out + (size_t)r * ldo + h * 64 + c * 8) = pack8(o8);
+    }
+}
+
+extern "C" hipError_t dlms_attention_split(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
+                                           const int* row_kvlen, void* out, int ldo, int R, int H, int t_max,
+                                           int n_slots, float scale, int nw, hipStream_t stream) {
+    if (R <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
+    const float sl2 = scale * 1.4426950408889634f;
+    auto go = [&](auto kern, int threads) {
+        hipLaunchKernelGGL(kern, dim3(H, R), dim3(threads), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
+                           reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
+                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, n_slots, sl2);
+    };
+    switch (nw) {
+        case 2: go(attn_split_kernel<2>, 128); break;
+        case 4: go(attn_split_kernel<4>, 256); break;
+        case 8: go(attn_split_kernel<8>, 512); break;
+        case 16: go(attn_split_kernel<16>, 1024); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+DLMS_CHECK_EXPORT(skinny)

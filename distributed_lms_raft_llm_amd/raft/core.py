@@ -438,7 +438,9 @@ class RaftCore:
             break
         last_new = prev + len(ents)
         if m.leader_commit > self.commit_index:
-            self.commit_index = min(m.leader_commit, last_new)
+            # monotone: a stale / duplicate AppendEntries with a short ``last_new`` must never move
+            # the commit index backwards (status(), read fences and a later election read it)
+            self.commit_index = max(self.commit_index, min(m.leader_commit, last_new))
         return AppendResponse(self.id, m.src, self.current_term, True, last_new)
 
     def _on_append_response(self, m: AppendResponse, now: float) -> list:

@@ -59,3 +59,31 @@ def test_bench_two_ranks_under_torchrun():
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
     assert d["new_tokens_per_step"] == 64.0  # summed over both ranks
     assert abs(d["value"] - 64.0 * 1000 / d["ms_per_step"]) / d["value"] < 0.05
+
+
+def test_bench_self_launches_ranks_without_torchrun():
+    """``bench.py --gpus 2`` with no launcher spawns its two ranks itself (before any GPU call)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS, "--latency-batches", ""], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    assert lines[0]["config"]["parallelism"] == "dp2" and lines[0]["new_tokens_per_step"] == 64.0
+
+
+def test_bench_rejects_mismatched_world_size():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", WORLD_SIZE="1")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_bench_reports_latency_points():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "bench.py", *ARGS, "--latency-batches", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_lines(p.stdout)[0]
+    assert d["p50_query_latency_ms_b1"] > 0 and d["tok_s_b1"] > 0

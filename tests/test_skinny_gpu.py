@@ -1,0 +1,231 @@
+"""Numerics of the latency-path kernels (ops/csrc/skinny.hip) against plain PyTorch fp32
+references: pre-shuffled-weight MFMA GEMMs for M <= 32 rows with their fused LayerNorm prologue
+and epilogues, and the split-K flash-decode attention (SURVEY.md §4.3 "Kernel unit")."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from distributed_lms_raft_llm_amd import ops
+
+    ops.lib()
+    return ops
+
+
+def _rand(*shape, scale=1.0, seed=0, dtype=torch.bfloat16):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+def _ln_ref(x, g, b, eps):
+    return torch.nn.functional.layer_norm(x, (x.shape[1],), g, b, eps)
+
+
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 32])
+@pytest.mark.parametrize("N,K", [(768, 768), (2304, 768), (3072, 1024), (4800, 1600)])
+def test_skinny_ln_bf16(M, N, K):
+    ops = _ops()
+    x = _rand(M, K, seed=1, dtype=torch.float32) * 3 + 0.5
+    g, b = _rand(K, seed=2, dtype=torch.float32), _rand(K, seed=3, dtype=torch.float32)
+    w = _rand(N, K, scale=0.05, seed=4)
+    bias = _rand(N, seed=5, dtype=torch.float32)
+    out = ops.skinny_gemm(x, ops.shuffle_weight(w), ops.EPI_BF16, ln=(g, b, 1e-5), bias=bias)
+    h = _ln_ref(x, g, b, 1e-5).to(torch.bfloat16).float()
+    ref = h @ w.float().t() + bias
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 8, 32])
+def test_skinny_ln_gelu(M):
+    ops = _ops()
+    N, K = 3072, 768
+    x = _rand(M, K, seed=11, dtype=torch.float32)
+    g, b = _rand(K, seed=12, dtype=torch.float32), _rand(K, seed=13, dtype=torch.float32)
+    w = _rand(N, K, scale=0.05, seed=14)
+    bias = _rand(N, seed=15, dtype=torch.float32) * 0.1
+    out = ops.skinny_gemm(x, ops.shuffle_weight(w), ops.EPI_GELU_TANH, ln=(g, b, 1e-5), bias=bias)
+    h = _ln_ref(x, g, b, 1e-5).to(torch.bfloat16).float()
+    ref = torch.nn.functional.gelu(h @ w.float().t() + bias, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 29])
+@pytest.mark.parametrize("N,K", [(768, 768), (768, 3072), (1024, 4096), (1600, 6400)])
+def test_skinny_residual_inplace(M, N, K):
+    ops = _ops()
+    a = _rand(M, K, seed=21)
+    w = _rand(N, K, scale=0.02, seed=22)
+    bias = _rand(N, seed=23, dtype=torch.float32)
+    x = _rand(M, N, seed=24, dtype=torch.float32)
+    ref = x + a.float() @ w.float().t() + bias
+    ops.skinny_gemm(a, ops.shuffle_weight(w), ops.EPI_F32, bias=bias, out=x)
+    torch.testing.assert_close(x, ref, atol=1e-2, rtol=1e-3)
+
+
+def test_skinny_partial():
+    ops = _ops()
+    M, N, K = 4, 768, 3072
+    a, w = _rand(M, K, seed=31), _rand(N, K, scale=0.02, seed=32)
+    out = ops.skinny_gemm(a, ops.shuffle_weight(w), ops.EPI_PARTIAL)
+    torch.testing.assert_close(out, a.float() @ w.float().t(), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 5, 32])
+def test_skinny_qkv_scatter(M):
+    ops = _ops()
+    H, T, S = 12, 40, 40
+    D = H * 64
+    x = _rand(M, D, seed=41, dtype=torch.float32)
+    g, b = _rand(D, seed=42, dtype=torch.float32), _rand(D, seed=43, dtype=torch.float32)
+    w = _rand(3 * D, D, scale=0.05, seed=44)
+    bias = _rand(3 * D, seed=45, dtype=torch.float32)
+    q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    gen = torch.Generator().manual_seed(46)
+    slot = torch.randperm(S, generator=gen)[:M].to(torch.int32).to(DEV)
+    pos = torch.randint(0, T, (M,), generator=gen).to(torch.int32).to(DEV)
+    ops.skinny_gemm(x, ops.shuffle_weight(w), ops.EPI_QKV, ln=(g, b, 1e-5), bias=bias, q_out=q, k_cache=kc,
+                    v_cache=vc, row_slot=slot, row_pos=pos)
+    h = _ln_ref(x, g, b, 1e-5).to(torch.bfloat16).float()
+    z = h @ w.float().t() + bias
+    torch.testing.assert_close(q.float(), z[:, :D], atol=3e-2, rtol=2e-2)
+    for r in range(M):
+        s, p = int(slot[r]), int(pos[r])
+        torch.testing.assert_close(kc[s, :, p].float().reshape(-1), z[r, D:2 * D], atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(vc[s, :, p].float().reshape(-1), z[r, 2 * D:], atol=3e-2, rtol=2e-2)
+    # nothing else written
+    mask = torch.zeros(S, T, dtype=torch.bool, device=DEV)
+    mask[slot.long(), pos.long()] = True
+    assert kc.permute(0, 2, 1, 3)[~mask].abs().sum() == 0
+
+
+@pytest.mark.parametrize("M", [1, 6, 32])
+def test_skinny_argmax_penalty(M):
+    """Keys equal the fp32 argmax of the penalised logits wherever the top-2 margin is clear."""
+    ops = _ops()
+    V, Vp, K = 3000, 3008 + 64, 768  # padded vocabulary: columns >= V never win
+    Vp = (Vp + 63) // 64 * 64
+    h = _rand(M, K, seed=51)
+    w = _rand(Vp, K, scale=0.05, seed=52)
+    words = Vp // 32
+    gen = torch.Generator().manual_seed(53)
+    seen_ids = [torch.randint(0, V, (20,), generator=gen) for _ in range(M)]
+    seen = torch.zeros(M, words, dtype=torch.int32)
+    for r, ids in enumerate(seen_ids):
+        for t in ids.tolist():
+            seen[r, t // 32] |= (1 << (t % 32)) if t % 32 < 31 else -(1 << 31)
+    seen = seen.to(DEV)
+    keys = torch.zeros(M, Vp // 64, dtype=torch.int64, device=DEV)
+    ops.skinny_gemm(h, ops.shuffle_weight(w), ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2)
+    tok = ops.argmax_reduce(keys)
+    idx = (~(tok & 0xFFFFFFFF)).to(torch.int64) & 0xFFFFFFFF
+    logits = h.float() @ w.float().t()
+    logits[:, V:] = -float("inf")
+    for r, ids in enumerate(seen_ids):
+        u = torch.unique(ids).to(DEV)
+        v = logits[r, u]
+        logits[r, u] = torch.where(v < 0, v * 1.2, v / 1.2)
+    top2 = logits.topk(2, dim=1)
+    clear = (top2.values[:, 0] - top2.values[:, 1]) > 1e-2
+    assert clear.any()
+    assert torch.equal(idx[clear].cpu(), top2.indices[clear, 0].cpu())
+
+
+def _attn_ref(q, kc, vc, slot, kvlen):
+    R = q.shape[0]
+    H = kc.shape[1]
+    out = torch.empty(R, H * 64, device=DEV)
+    for r in range(R):
+        s, n = int(slot[r]), int(kvlen[r])
+        k = kc[s, :, :n].float()  # [H, n, 64]
+        v = vc[s, :, :n].float()
+        qq = q[r].float().reshape(H, 1, 64)
+        p = torch.softmax((qq @ k.transpose(1, 2)) / 8.0, dim=-1)
+        out[r] = (p @ v).reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("B,T", [(1, 1024), (8, 1024), (3, 150), (16, 37)])
+@pytest.mark.parametrize("waves", [2, 4, 16])
+def test_attention_split(B, T, waves):
+    ops = _ops()
+    H, S = 12, max(B, 4)
+    kc = _rand(S, H, T, 64, seed=61)
+    vc = _rand(S, H, T, 64, seed=62)
+    q = _rand(B, H * 64, seed=63)
+    gen = torch.Generator().manual_seed(64)
+    slot = torch.randperm(S, generator=gen)[:B].to(torch.int32).to(DEV)
+    kvlen = torch.randint(1, T + 1, (B,), generator=gen)
+    kvlen[0] = T
+    kvlen = kvlen.to(torch.int32).to(DEV)
+    out = ops.attention_split(q, kc, vc, slot, kvlen, waves=waves)
+    ref = _attn_ref(q, kc, vc, slot, kvlen)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_attention_split_matches_wave_kernel():
+    """Split-K and the one-wave-per-(row, head) kernel agree (same online-softmax numerics)."""
+    ops = _ops()
+    B, H, T = 5, 12, 150
+    kc, vc = _rand(B, H, T, 64, seed=71), _rand(B, H, T, 64, seed=72)
+    q = _rand(B, H * 64, seed=73)
+    slot = torch.arange(B, dtype=torch.int32, device=DEV)
+    kvlen = torch.tensor([1, 9, 64, 100, 150], dtype=torch.int32, device=DEV)
+    a = ops.attention_split(q, kc, vc, slot, kvlen, waves=8)
+    b = ops.row_attention(q, kc, vc, slot, kvlen)
+    torch.testing.assert_close(a.float(), b.float(), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4, 5, 8])
+@pytest.mark.parametrize("K", [768, 1024, 1280, 1600])
+@pytest.mark.parametrize("nsplit", [0, 1, 4])
+def test_skinny_addln_gelu(M, K, nsplit):
+    """v = x + res_bias + sum(parts); x_out = v; out = gelu(LN(v) @ W.T + b)."""
+    ops = _ops()
+    if M > ops.skinny_addln_max_rows(K):
+        pytest.skip("row count above this width's fused-kernel limit")
+    N = 4 * K
+    x = _rand(M, K, seed=81, dtype=torch.float32)
+    parts = _rand(4, M, K, seed=82, dtype=torch.float32)
+    rb = _rand(K, seed=83, dtype=torch.float32)
+    g, b = _rand(K, seed=84, dtype=torch.float32), _rand(K, seed=85, dtype=torch.float32)
+    w = _rand(N, K, scale=0.05, seed=86)
+    bias = _rand(N, seed=87, dtype=torch.float32) * 0.1
+    x_out = torch.full_like(x, 7.0)
+    out = ops.skinny_addln_gemm(x, ops.shuffle_weight(w), ops.EPI_GELU_TANH, g, b, 1e-5, x_out=x_out, parts=parts,
+                                nsplit=nsplit, res_bias=rb, bias=bias)
+    v = x + rb + parts[:nsplit].sum(0)
+    torch.testing.assert_close(x_out, v, atol=1e-5, rtol=1e-5)
+    h = _ln_ref(v, g, b, 1e-5).to(torch.bfloat16).float()
+    ref = torch.nn.functional.gelu(h @ w.float().t() + bias, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+def test_skinny_addln_qkv(M):
+    ops = _ops()
+    H, T, S = 12, 20, 16
+    D = 64 * H
+    x = _rand(M, D, seed=91, dtype=torch.float32)
+    g, b = _rand(D, seed=92, dtype=torch.float32), _rand(D, seed=93, dtype=torch.float32)
+    w = _rand(3 * D, D, scale=0.05, seed=94)
+    bias = _rand(3 * D, seed=95, dtype=torch.float32)
+    q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    slot = torch.arange(M, dtype=torch.int32, device=DEV) * 2
+    pos = torch.arange(M, dtype=torch.int32, device=DEV) + 3
+    ops.skinny_addln_gemm(x, ops.shuffle_weight(w), ops.EPI_QKV, g, b, 1e-5, bias=bias, q_out=q, k_cache=kc,
+                          v_cache=vc, row_slot=slot, row_pos=pos)
+    h = _ln_ref(x, g, b, 1e-5).to(torch.bfloat16).float()
+    z = h @ w.float().t() + bias
+    torch.testing.assert_close(q.float(), z[:, :D], atol=3e-2, rtol=2e-2)
+    for r in range(M):
+        s, p = int(slot[r]), int(pos[r])
+        torch.testing.assert_close(kc[s, :, p].float().reshape(-1), z[r, D:2 * D], atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(vc[s, :, p].float().reshape(-1), z[r, 2 * D:], atol=3e-2, rtol=2e-2)

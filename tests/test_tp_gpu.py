@@ -74,5 +74,17 @@ def test_tp2_on_one_gpu_matches_tp1(p2p):
         cos = torch.nn.functional.cosine_similarity(torch.from_numpy(r[2]), ref_hid, dim=-1)
         assert bool((cos > 0.999).all()), cos
         assert r[3] == res[0][3]
-    agree = [sum(a == b for a, b in zip(x, y)) / max(len(x), 1) for x, y in zip(res[0][3], ref_out)]
-    assert all(a > 0.5 for a in agree), agree
+    # margin-aware exactness against the fp32 oracle (teacher-forced on each engine's own output):
+    # TP=2 and TP=1 must both pick the oracle's greedy token wherever it is decisive
+    from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, teacher_forced_check
+
+    oracle = GPT2Reference(cfg, w, device="cuda")
+    for outs in (res[0][3], ref_out):
+        decisive = total = 0
+        for o, p in zip(outs, prompts):
+            assert o[: len(p)] == p
+            r = teacher_forced_check(oracle, o, len(p), 1.2, eps=0.05)
+            assert not r["mismatches"], r["mismatches"]
+            decisive += r["decisive"]
+            total += r["positions"]
+        assert decisive >= 0.7 * total, (decisive, total)
