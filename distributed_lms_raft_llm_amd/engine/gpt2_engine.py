@@ -96,6 +96,7 @@ class _Rows:
     tiles: "ops.AttnTiles | None" = None  # packed prompts: MFMA tile attention instead of per-row
     split_cap: int = 8  # split-K cap of the row-parallel projections (lower for concurrent row parts)
     split_fixed: int | None = None  # pinned split-K (M-independent arithmetic: prefill_split)
+    persist_attn: bool = False  # decode attention as the low-occupancy persistent kernel
 
 
 class HostResult:
@@ -135,6 +136,7 @@ class HipGPT2Engine:
     # split-K of the row-parallel projections on the latency path (fixed: the fused add+LN
     # kernel sums exactly this many slabs)
     SMALL_SPLIT = 4
+    PS_LM_MIN_ROWS = 256
 
     def __init__(self, cfg: GPT2Config, weights: dict[str, torch.Tensor] | GPT2DeviceWeights, device=None,
                  max_batch: int | str = 256, max_length: int = 150, tp_group=None, use_graph: bool = True,
@@ -204,6 +206,10 @@ class HipGPT2Engine:
         # profiles/r1_split_cap_insitu.log; DLMS_OVERLAP_SPLIT_CAP overrides.
         self.overlap_split_cap = int(os.environ.get("DLMS_OVERLAP_SPLIT_CAP", "2"))
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
+        # overlapped step's attention: persistent grid of this many 4-wave workgroups (0 = one wave
+        # per (row, head) pair, the default: 256/512/1024 blocks measured -6 % / +0.3 % / +1 %, i.e.
+        # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
+        self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "0"))
         if self.overlap_parts not in (2, 3, 4):
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
         if latency_path is None:
@@ -216,6 +222,12 @@ class HipGPT2Engine:
                 if lw.w_qkv_sh is None:
                     lw.w_qkv_sh = ops.shuffle_weight(lw.w_qkv)
                     lw.w_fc_sh = ops.shuffle_weight(lw.w_fc)
+        # LM head of the throughput path (>= PS_LM_MIN_ROWS rows): panel-resident gemm_ps on a
+        # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
+        # (profiles/r2_gemm_ps_vs_tiled.log)
+        self.lm_head_sh = None
+        if not self.w.fp8 and self.max_batch >= self.PS_LM_MIN_ROWS and os.environ.get("DLMS_PS_LMHEAD", "1") != "0":
+            self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -281,13 +293,13 @@ class HipGPT2Engine:
             else:
                 dist.all_reduce(t, group=self.tp_group)
 
-    def _gather_keys(self, B: int) -> torch.Tensor:
+    def _gather_keys(self, B: int, P: int) -> torch.Tensor:
         """Argmax keys as a [B, P] view: the LM head's per-tile partials (TP=1), or one reduced key
         per vocab shard after an all-gather of 8 B per row per rank (TP>1)."""
         if self.tp_size > 1:
             import torch.distributed as dist
 
-            ops.argmax_reduce(self.key_parts[:B], out=self.local_keys[:B])
+            ops.argmax_reduce(self.key_parts[:B, :P], out=self.local_keys[:B])
             flat = self.all_keys.view(-1)[: self.tp_size * B]
             if self.xgmi is not None:
                 self.xgmi.all_gather_u64(self.local_keys[:B], flat.view(self.tp_size, B))
@@ -299,7 +311,7 @@ class HipGPT2Engine:
                 for i, p in enumerate(parts):
                     flat.view(self.tp_size, B)[i].copy_(p)
             return flat.view(self.tp_size, B).t()
-        return self.key_parts[:B]
+        return self.key_parts[:B, :P]
 
     # ------------------------------------------------------------------ transformer body
     def _split(self, M: int, N: int, K: int, cap: int = 8) -> int:
@@ -368,6 +380,10 @@ class HipGPT2Engine:
             # decode with few (row, head) pairs: split-K flash-decode puts NW waves on each pair's keys
             ops.attention_split(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
                                 waves=ops.attention_split_waves(self.max_length))
+        elif r.persist_attn:
+            # overlapped step: a fixed low-occupancy grid leaves wave slots to the other half's GEMMs
+            ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
+                              impl="persist", blocks=self.persist_attn_blocks)
         else:  # decode (K5): one query per sequence, a pure KV stream
             ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att)
 
@@ -414,7 +430,12 @@ class HipGPT2Engine:
         cfg = self.cfg
         hi = lo + B
         seen_rows = self.seen[lo:hi] if seen is None else seen
-        if hidden.dtype == ops.FP8:
+        P = self.key_parts.shape[1]  # partial keys per row the LM head writes (and the consumer reads)
+        if hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B >= self.PS_LM_MIN_ROWS:
+            P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16)
+            ops.gemm_ps(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
+                        vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
+        elif hidden.dtype == ops.FP8:
             ops.gemm(hidden, self.w.lm_head8, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                      vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty, a_scale=hscale,
                      w_scale=self.w.s_lm)
@@ -424,9 +445,9 @@ class HipGPT2Engine:
         if lo:
             if self.tp_size > 1:
                 raise ValueError("row-offset LM head is TP=1 only")
-            keys = self.key_parts[lo:hi]
+            keys = self.key_parts[lo:hi, :P]
         else:
-            keys = self._gather_keys(B)
+            keys = self._gather_keys(B, P)
         if slot_map is None:
             ops.decode_update(keys, self.lens[lo:hi], self.finished[lo:hi], self.out_tokens[lo:hi],
                               self.seen[lo:hi], self.cur_tok[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi],
@@ -446,6 +467,7 @@ class HipGPT2Engine:
                           self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], hi - lo,
                           self.h8[lo:hi] if fp8 else None, self.hsc[lo:hi] if fp8 else None)
         r.split_cap = self.overlap_split_cap
+        r.persist_attn = self.persist_attn_blocks > 0
         return r
 
     def _part_step(self, r: "_Rows", lo: int, penalty: float):

@@ -27,11 +27,11 @@ LIB_DIR = _HERE / "_lib"
 LIB_PATH = LIB_DIR / "libdlms_hip.so"
 # debug variant: device-side range checks on every data-dependent index (common.h, DLMS_DEVICE_CHECKS)
 CHECKED_LIB_PATH = LIB_DIR / "libdlms_hip_checked.so"
-CHECK_UNITS = ("gemm", "attention", "decode", "encoder", "skinny")
+CHECK_UNITS = ("gemm", "attention", "decode", "encoder", "skinny", "gemm_ps")
 CHECK_SITES = {1: "embed token id", 2: "position id", 3: "decode_update slot_map", 4: "decode_update token id",
                5: "decode_update sequence length", 6: "seen_set row", 7: "QKV scatter slot", 8: "QKV scatter position",
                9: "attention slot", 10: "BERT token id", 11: "seen_set token id"}
-SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip", "skinny.hip"]
+SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip", "skinny.hip", "gemm_ps.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
 EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
@@ -133,6 +133,8 @@ def _bind(L):
         "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
                                    ctypes.POINTER(GemmEpi), P],
         "dlms_skinny_addln_max_rows": [I],
+        "dlms_gemm_ps": [I, P, I, P, I, I, I, I, I, I, I, ctypes.POINTER(GemmEpi), P],
+        "dlms_attention_persist": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, P],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -458,7 +460,7 @@ def layernorm_gather(x: torch.Tensor, rows: torch.Tensor, gamma, beta, eps: floa
 
 def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
                   row_kvlen: torch.Tensor, out: torch.Tensor | None = None, scale: float | None = None,
-                  impl: str = "wave"):
+                  impl: str = "wave", blocks: int = 512):
     """q: bf16 [R, H*64]; caches bf16 [slots, H, t_max, 64]; row r attends keys [0, row_kvlen[r]).
     impl "wave": one wave per (row, head), online softmax (default); "lds": block per (row, head),
     exact two-pass softmax through LDS (t_max <= 2048)."""
@@ -477,6 +479,11 @@ def row_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
         out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=q.device)
     _req(out, torch.bfloat16, "out", 2)
     sc = (1.0 / 8.0) if scale is None else scale
+    if impl == "persist":  # fixed low-occupancy grid looping over (row, head) pairs
+        _check(lib().dlms_attention_persist(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
+                                            _p(out), out.stride(0), R, H, T, S, float(sc), int(blocks), _stream()),
+               "attention_persist")
+        return out
     fn = lib().dlms_attention if impl == "wave" else lib().dlms_row_attention
     _check(fn(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen), _p(out), out.stride(0), R, H,
               T, S, float(sc), _stream()), "attention")
@@ -889,3 +896,106 @@ def attention_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                                       _p(out), out.stride(0), R, H, T, S, float(sc), int(waves), _stream()),
            "attention_split")
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Throughput-path decode GEMM: LDS-resident activation panel, pre-shuffled weights -> VGPRs
+# ---------------------------------------------------------------------------------------------
+PS_WAVES = 8
+
+
+def gemm_ps_geometry(M: int, N: int, epi: int, split: int = 1, cus: int = 256):
+    """(mt, nt, col_wgs) for ``gemm_ps``: 64-row blocks when the LM head's weight reuse matters
+    (and the panel fits), else 32; column workgroups sized so the grid covers the CUs about once
+    (the LM head loops over its tiles inside each wave)."""
+    mt = 4 if (epi == EPI_ARGMAX or M >= 512) else 2
+    nt = 2
+    row_blocks = -(-M // (16 * mt))
+    tiles = N // (16 * nt)
+    need = -(-tiles // PS_WAVES)  # column workgroups for one tile per wave
+    per_row = max(1, cus // max(1, row_blocks * split))
+    col_wgs = min(need, per_row) if epi == EPI_ARGMAX else need
+    return mt, nt, max(1, col_wgs)
+
+
+def gemm_ps(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, bias=None, out=None, q_out=None, k_cache=None,
+            v_cache=None, row_slot=None, row_pos=None, argmax_out=None, seen=None, vocab: int = 0,
+            col_offset: int = 0, penalty: float = 1.0, split_k: int = 1, geometry=None):
+    """C = a @ W.T for a ``shuffle_weight`` weight with the activation panel resident in LDS
+    (``gemm_ps.hip``).  Same epilogue contract as ``gemm`` except EPI_ARGMAX: one key per
+    (row, wave slot) -> ``argmax_out`` needs >= 8 * col_wgs columns (``gemm_ps_key_slots``)."""
+    _req(a, torch.bfloat16, "a", 2)
+    _req(w_sh, torch.bfloat16, "w_sh", 4)
+    if w_sh.shape[2] != 64 or w_sh.shape[3] != 8 or not w_sh.is_contiguous():
+        raise ValueError("gemm_ps: w_sh must be a contiguous shuffle_weight() tensor")
+    N, K = w_sh.shape[0] * 16, w_sh.shape[1] * 32
+    M = a.shape[0]
+    if a.shape[1] != K or a.stride(0) % 8 or a.data_ptr() % 16:
+        raise ValueError(f"gemm_ps: a {tuple(a.shape)} vs K={K} (16-byte aligned rows)")
+    if split_k < 1 or K % split_k or (K // split_k) % 128:
+        raise ValueError("gemm_ps: K / split_k must be a multiple of 128")
+    if epi != EPI_PARTIAL and split_k != 1:
+        raise ValueError("gemm_ps: split_k only with EPI_PARTIAL")
+    mt, nt, col_wgs = geometry or gemm_ps_geometry(M, N, epi, split_k)
+    if N % (16 * nt):
+        raise ValueError("gemm_ps: N must be a multiple of 16 * nt")
+    ep = GemmEpi()
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() < N:
+            raise ValueError("bias too short")
+        ep.bias = bias.data_ptr()
+    if epi in (EPI_BF16, EPI_GELU_TANH):
+        if out is None:
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+        _req(out, torch.bfloat16, "out", 2)
+        if out.shape[0] < M or out.shape[1] < N or out.stride(0) % 8 or out.data_ptr() % 16:
+            raise ValueError("gemm_ps: out too small / misaligned")
+        ep.out, ep.ldo = out.data_ptr(), out.stride(0)
+    elif epi == EPI_PARTIAL:
+        if out is None:
+            out = torch.empty(split_k, M, N, dtype=torch.float32, device=a.device)
+        _req(out, torch.float32, "out", 3)
+        if out.shape[0] < split_k or out.shape[1] < M or out.shape[2] < N or out.stride(1) % 4 or \
+                out.stride(0) % 4 or out.data_ptr() % 16:
+            raise ValueError("gemm_ps: partial out too small / misaligned")
+        ep.out, ep.ldo, ep.split_k, ep.split_stride = out.data_ptr(), out.stride(1), split_k, out.stride(0)
+    elif epi == EPI_QKV:
+        for t, n in ((q_out, "q_out"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+            _req(t, torch.bfloat16, n)
+        _req(row_slot, torch.int32, "row_slot", 1)
+        _req(row_pos, torch.int32, "row_pos", 1)
+        if N % 3 or (N // 3) % 64:
+            raise ValueError("QKV N must be 3 * d_local (64-wide heads)")
+        d_local = N // 3
+        if k_cache.dim() != 4 or k_cache.shape != v_cache.shape or k_cache.shape[1] * 64 != d_local or \
+                k_cache.shape[3] != 64 or not k_cache.is_contiguous() or not v_cache.is_contiguous():
+            raise ValueError(f"cache shape {tuple(k_cache.shape)} incompatible with d_local={d_local}")
+        if q_out.shape[0] < M or q_out.shape[1] < d_local or row_slot.numel() < M or row_pos.numel() < M or \
+                q_out.stride(0) % 8 or q_out.data_ptr() % 16:
+            raise ValueError("qkv epilogue buffers too small / misaligned")
+        ep.q_out, ep.ldq = q_out.data_ptr(), q_out.stride(0)
+        ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
+        ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
+        ep.n_heads, ep.t_max, ep.d_local, ep.n_slots = k_cache.shape[1], k_cache.shape[2], d_local, k_cache.shape[0]
+        out = q_out
+    elif epi == EPI_ARGMAX:
+        _req(argmax_out, torch.int64, "argmax_out", 2)
+        _req(seen, torch.int32, "seen", 2)
+        slots = PS_WAVES * col_wgs
+        if argmax_out.shape[0] < M or argmax_out.shape[1] < slots or seen.shape[0] < M or \
+                seen.shape[1] * 32 < vocab or col_offset % 64:
+            raise ValueError("gemm_ps argmax buffers too small / misaligned shard")
+        ep.argmax_out, ep.ldo, ep.seen = argmax_out.data_ptr(), argmax_out.stride(0), seen.data_ptr()
+        ep.seen_words, ep.vocab, ep.col_offset, ep.penalty = seen.stride(0), vocab, col_offset, penalty
+        out = argmax_out
+    else:
+        raise ValueError(f"gemm_ps: unsupported epilogue {epi}")
+    _check(lib().dlms_gemm_ps(epi, _p(a), a.stride(0), _p(w_sh), M, N, K, split_k, mt, nt, col_wgs, ctypes.byref(ep),
+                              _stream()), "dlms_gemm_ps")
+    return out
+
+
+def gemm_ps_key_slots(M: int, N: int) -> int:
+    """argmax_out columns ``gemm_ps(..., EPI_ARGMAX)`` writes for an M x N LM head."""
+    return PS_WAVES * gemm_ps_geometry(M, N, EPI_ARGMAX)[2]

@@ -203,6 +203,109 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
     }
 }
 
+// Persistent, low-occupancy variant of attn_wave_kernel for the overlapped decode step: a fixed
+// grid of NB workgroups x 4 waves, each wave looping over (row, head) pairs (consecutive pairs = the
+// heads of one row, adjacent in the cache).  An 8-deep unroll keeps 16 KiB of K/V in flight per wave
+// so ~8 waves per CU still stream HBM at full rate -- and leave the CU's other wave slots, LDS and
+// MFMA pipes to the GEMMs of the other row half running on the second stream (a one-wave-per-pair
+// grid of 6k waves occupies every slot and serialises the two streams at kernel granularity).
+template <int U>
+__global__ __launch_bounds__(256) void attn_persist_kernel(const bf16_t* __restrict__ q, int ldq,
+                                                           const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                                           const int* __restrict__ row_slot,
+                                                           const int* __restrict__ row_kvlen, bf16_t* out, int ldo,
+                                                           int R, int H, int t_max, int n_slots, float scale_log2) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3;
+    const int c = lane & 7;
+    const int nwaves = gridDim.x * 4;
+    const int npairs = R * H;
+    for (int pair = blockIdx.x * 4 + (threadIdx.x >> 6); pair < npairs; pair += nwaves) {
+        const int r = pair / H, h = pair - r * H;
+        const int slot = (int)dlms_idx(row_slot[r], n_slots, CHK_ATTN_SLOT);
+        int kvlen = row_kvlen[r];
+        kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
+        const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+        const bf16_t* K = kc + head_off + c * 8;
+        const bf16_t* V = vc + head_off + c * 8;
+        float qf[8];
+        unpack8(*reinterpret_cast<const uint4*>(q + (size_t)r * ldq + h * 64 + c * 8), qf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[j] *= scale_log2;
+        float m = -INFINITY, l = 0.f;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int t0 = 0; t0 < kvlen; t0 += 8 * U) {
+            uint4 kr[U], vr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int t = t0 + u * 8 + g;
+                t = t < kvlen ? t : kvlen - 1;
+                const u32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(K + (size_t)t * 64));
+                const u32x4_t b = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(V + (size_t)t * 64));
+                kr[u] = make_uint4(a.x, a.y, a.z, a.w);
+                vr[u] = make_uint4(b.x, b.y, b.z, b.w);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float kf[8];
+                unpack8(kr[u], kf);
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
+                s += __shfl_xor(s, 1, 64);
+                s += __shfl_xor(s, 2, 64);
+                s += __shfl_xor(s, 4, 64);
+                if (t0 + u * 8 + g < kvlen) {
+                    const float m_new = fmaxf(m, s);
+                    const float corr = exp2f(m - m_new);
+                    const float p = exp2f(s - m_new);
+                    float vf[8];
+                    unpack8(vr[u], vf);
+                    l = l * corr + p;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[j] = acc[j] * corr + p * vf[j];
+                    m = m_new;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+            const float m_o = __shfl_xor(m, o, 64);
+            const float l_o = __shfl_xor(l, o, 64);
+            const float m_n = fmaxf(m, m_o);
+            const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
+            const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
+            l = l * a + l_o * b;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x_o = __shfl_xor(acc[j], o, 64);
+                acc[j] = acc[j] * a + x_o * b;
+            }
+            m = m_n;
+        }
+        if (g == 0) {
+            const float inv = 1.f / l;
+            float o8[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o8[j] = acc[j] * inv;
+            *reinterpret_cast<uint4*>(out + (size_t)r * ldo + h * 64 + c * 8) = pack8(o8);
+        }
+    }
+}
+
+extern "C" hipError_t dlms_attention_persist(const void* q, int ldq, const void* kc, const void* vc,
+                                             const int* row_slot, const int* row_kvlen, void* out, int ldo, int R,
+                                             int H, int t_max, int n_slots, float scale, int blocks,
+                                             hipStream_t stream) {
+    if (R <= 0 || H <= 0 || t_max <= 0 || blocks <= 0) return hipErrorInvalidValue;
+    const int need = (R * H + 3) / 4;
+    hipLaunchKernelGGL(attn_persist_kernel<8>, dim3(blocks < need ? blocks : need), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
+                       reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, reinterpret_cast<bf16_t*>(out), ldo,
+                       R, H, t_max, n_slots, scale * 1.4426950408889634f);
+    return hipGetLastError();
+}
+
 // Default: 4-deep unroll with non-temporal K/V loads (the cache is streamed once per layer; keeping
 // it out of L2/MALL leaves them to the weights): +6 % whole-step at 1024 queries, +4.5 % at 256
 // (profiles/r1_attention_variants.log, in-situ A/B in profiles/r1_bench_lines.jsonl).

@@ -229,3 +229,91 @@ def test_skinny_addln_qkv(M):
         s, p = int(slot[r]), int(pos[r])
         torch.testing.assert_close(kc[s, :, p].float().reshape(-1), z[r, D:2 * D], atol=3e-2, rtol=2e-2)
         torch.testing.assert_close(vc[s, :, p].float().reshape(-1), z[r, 2 * D:], atol=3e-2, rtol=2e-2)
+
+
+# ---------------------------------------------------------------------------------------------
+# gemm_ps: LDS-resident activation panel + pre-shuffled weights (throughput path)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("M", [1, 40, 64, 100, 512])
+@pytest.mark.parametrize("geo", [(2, 1, None), (2, 2, None), (4, 2, None), (4, 1, 3)])
+def test_gemm_ps_bf16_gelu(M, geo):
+    ops = _ops()
+    N, K = 1024, 768
+    a, w = _rand(M, K, seed=101), _rand(N, K, scale=0.05, seed=102)
+    bias = _rand(N, seed=103, dtype=torch.float32) * 0.1
+    mt, nt, cw = geo
+    cw = cw or -(-(N // (16 * nt)) // 8)
+    out = ops.gemm_ps(a, ops.shuffle_weight(w), ops.EPI_GELU_TANH, bias=bias, geometry=(mt, nt, cw))
+    ref = torch.nn.functional.gelu(a.float() @ w.float().t() + bias, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,K,split", [(64, 768, 1), (300, 768, 2), (512, 3072, 4), (37, 1024, 1)])
+def test_gemm_ps_partial(M, K, split):
+    ops = _ops()
+    N = 768
+    a, w = _rand(M, K, seed=111), _rand(N, K, scale=0.02, seed=112)
+    out = ops.gemm_ps(a, ops.shuffle_weight(w), ops.EPI_PARTIAL, split_k=split)
+    torch.testing.assert_close(out.sum(0), a.float() @ w.float().t(), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M", [5, 512])
+def test_gemm_ps_qkv(M):
+    ops = _ops()
+    H, T, S = 12, 8, 600
+    D = 64 * H
+    a, w = _rand(M, D, seed=121), _rand(3 * D, D, scale=0.05, seed=122)
+    bias = _rand(3 * D, seed=123, dtype=torch.float32)
+    q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    slot = torch.randperm(S, generator=torch.Generator().manual_seed(1))[:M].to(torch.int32).to(DEV)
+    pos = torch.randint(0, T, (M,), generator=torch.Generator().manual_seed(2)).to(torch.int32).to(DEV)
+    ops.gemm_ps(a, ops.shuffle_weight(w), ops.EPI_QKV, bias=bias, q_out=q, k_cache=kc, v_cache=vc, row_slot=slot,
+                row_pos=pos)
+    z = a.float() @ w.float().t() + bias
+    torch.testing.assert_close(q.float(), z[:, :D], atol=3e-2, rtol=2e-2)
+    ks = kc[slot.long(), :, pos.long()].float().reshape(M, -1)
+    vs = vc[slot.long(), :, pos.long()].float().reshape(M, -1)
+    torch.testing.assert_close(ks, z[:, D:2 * D], atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(vs, z[:, 2 * D:], atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [3, 64, 512])
+def test_gemm_ps_argmax_matches_tiled(M):
+    """Same keys as the tiled LM head's fused penalty + argmax (identical per-element sums are not
+    required: compare the decoded token wherever the fp32 top-2 margin is clear)."""
+    ops = _ops()
+    V, K = 50257, 768
+    Vp = 50304
+    h = _rand(M, K, seed=131)
+    w = _rand(Vp, K, scale=0.05, seed=132)
+    seen = torch.randint(-2**31, 2**31 - 1, (M, Vp // 32), generator=torch.Generator().manual_seed(3),
+                         dtype=torch.int64).to(torch.int32).to(DEV)
+    seen &= 0x01010101  # ~1/8 of the vocabulary penalised
+    keys = torch.zeros(M, ops.gemm_ps_key_slots(M, Vp), dtype=torch.int64, device=DEV)
+    ops.gemm_ps(h, ops.shuffle_weight(w), ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2)
+    tok = ops.argmax_reduce(keys)
+    got = ((~(tok & 0xFFFFFFFF)) & 0xFFFFFFFF).cpu()
+    logits = h.float() @ w.float().t()
+    bits = ((seen.long().unsqueeze(-1) >> torch.arange(32, device=DEV)) & 1).reshape(M, -1).bool()
+    logits = torch.where(bits, torch.where(logits < 0, logits * 1.2, logits / 1.2), logits)
+    logits[:, V:] = -float("inf")
+    top2 = logits.topk(2, dim=1)
+    clear = (top2.values[:, 0] - top2.values[:, 1]) > 1e-2
+    assert clear.float().mean() > 0.5
+    assert torch.equal(got[clear.cpu()], top2.indices[clear, 0].cpu())
+
+
+@pytest.mark.parametrize("blocks", [1, 7, 512])
+def test_attention_persist_matches_reference(blocks):
+    """The persistent low-occupancy decode attention (fixed grid looping over (row, head) pairs)."""
+    ops = _ops()
+    B, H, T, S = 37, 12, 150, 40
+    kc, vc = _rand(S, H, T, 64, seed=141), _rand(S, H, T, 64, seed=142)
+    q = _rand(B, H * 64, seed=143)
+    gen = torch.Generator().manual_seed(144)
+    slot = torch.randperm(S, generator=gen)[:B].to(torch.int32).to(DEV)
+    kvlen = torch.randint(1, T + 1, (B,), generator=gen).to(torch.int32).to(DEV)
+    out = ops.row_attention(q, kc, vc, slot, kvlen, impl="persist", blocks=blocks)
+    torch.testing.assert_close(out.float(), _attn_ref(q, kc, vc, slot, kvlen), atol=2e-2, rtol=2e-2)
