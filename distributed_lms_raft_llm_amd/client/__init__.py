@@ -5,11 +5,17 @@ The GUI discovers the leader by polling ``RaftService.WhoIsLeader`` (5 rounds x 
 apart, no deadlines) before EVERY action (``lms_gui_final.py:64-185``).  ``LMSClient`` caches the
 leader, re-discovers it only when a call fails with UNAVAILABLE / DEADLINE_EXCEEDED, and retries
 the call, so a leader crash costs one election (~0.2-0.3 s here) instead of minutes.
+
+Writes (Register, Post, GradeAssignment, RespondToQuery, Logout) carry a client request id
+(``x-dlms-request-id`` metadata) that is the same on every retry of one logical call; the state
+machine applies an id once (``lms/commands.py``), so retrying a write whose first attempt committed
+before its reply was lost can never post twice or answer the student's NEXT query.
 """
 from __future__ import annotations
 
 import os
 import time
+import uuid
 
 import grpc
 
@@ -59,13 +65,17 @@ class LMSClient:
             time.sleep(0.05)
         raise NoLeader(f"no leader among {self.addresses}")
 
+    WRITES = {"Register", "Post", "GradeAssignment", "RespondToQuery", "Logout"}
+
     def call(self, method: str, request, timeout: float | None = None, service: str = "LMS"):
         end = time.time() + self.discover_timeout
         avoid = None
+        md = (("x-dlms-request-id", uuid.uuid4().hex),) if method in self.WRITES else None
         while True:
             addr = self.leader_address or self.discover(avoid)
             try:
-                return getattr(wire.Stub(service, self._ch(addr)), method)(request, timeout=timeout or self.timeout)
+                return getattr(wire.Stub(service, self._ch(addr)), method)(request, timeout=timeout or self.timeout,
+                                                                           metadata=md)
             except grpc.RpcError as e:
                 if e.code() not in RETRYABLE or time.time() >= end:
                     raise

@@ -18,8 +18,14 @@ GradeAssignment        [student, grade]                                lms_serve
 
 Additional operations of this implementation (new ``operation`` values, format unchanged):
 ``NoOp`` (leader's first entry of a term), ``Login`` [username, token, role] / ``Logout``
-[token] (sessions survive leader failover), ``StoreBlob`` [filename, sha256, base64] (uploads
-replicate with the log) and ``SetVal`` [key, value] (the RaftService debug KV API).
+[token] (sessions survive leader failover), ``PutBlob`` [filename, sha256, size] (an upload the
+leader pre-replicated to a majority over ``FileTransferService.SendFile``: lms/blobs.py), the
+legacy ``StoreBlob`` [filename, sha256, base64] (still applied when replaying old logs) and
+``SetVal`` [key, value] (the RaftService debug KV API).
+
+An optional top-level ``"rid"`` (client request id) makes a write idempotent: the state machine
+applies a given rid once and answers retries with the first result (a client that retries a
+write after a leader failover must not post the same assignment twice).
 
 ``decode`` also accepts the reference's shadowed legacy encoder (``lms_server.py:317-333``):
 ``Op arg1 "multi word arg" ...`` (shlex quoting).
@@ -37,7 +43,7 @@ REFERENCE_OPS = {
     "RespondToQuery": 3,
     "GradeAssignment": 2,
 }
-EXTRA_OPS = {"NoOp": 0, "Login": 3, "Logout": 1, "StoreBlob": 3, "SetVal": 2}
+EXTRA_OPS = {"NoOp": 0, "Login": 3, "Logout": 1, "PutBlob": 3, "StoreBlob": 3, "SetVal": 2}
 ALL_OPS = {**REFERENCE_OPS, **EXTRA_OPS}
 
 
@@ -45,29 +51,38 @@ class BadCommand(ValueError):
     pass
 
 
-def encode(operation: str, args: list) -> str:
+def encode(operation: str, args: list, rid: str | None = None) -> str:
     if operation not in ALL_OPS:
         raise BadCommand(f"unknown operation {operation!r}")
     if len(args) != ALL_OPS[operation]:
         raise BadCommand(f"{operation} takes {ALL_OPS[operation]} args, got {len(args)}")
-    return json.dumps({"operation": operation, "args": list(args)})
+    obj = {"operation": operation, "args": list(args)}
+    if rid:
+        obj["rid"] = str(rid)
+    return json.dumps(obj)
 
 
 def decode(command: str) -> tuple[str, list]:
+    op, args, _ = decode_full(command)
+    return op, args
+
+
+def decode_full(command: str) -> tuple[str, list, str | None]:
+    """(operation, args, request id or None)."""
     s = command.strip()
     if s.startswith("{"):
         try:
             obj = json.loads(s)
         except ValueError as e:
             raise BadCommand(f"malformed JSON command: {e}") from e
-        op, args = obj.get("operation"), obj.get("args", [])
+        op, args, rid = obj.get("operation"), obj.get("args", []), obj.get("rid")
         if not isinstance(op, str) or not isinstance(args, list):
             raise BadCommand("command must carry a string 'operation' and a list 'args'")
-        return op, args
+        return op, args, (str(rid) if rid else None)
     try:
         parts = shlex.split(s)
     except ValueError as e:
         raise BadCommand(f"malformed legacy command: {e}") from e
     if not parts:
         raise BadCommand("empty command")
-    return parts[0], parts[1:]
+    return parts[0], parts[1:], None

@@ -60,23 +60,34 @@ def _text_from_content(content: bytes) -> str:
     return "\n".join(p.strip("\n") for p in pieces if p.strip())
 
 
-def _builtin_extract(data: bytes) -> str:
-    texts = []
-    for raw in _STREAM.findall(data):
+def _builtin_extract(data: bytes, limit: int | None = None) -> str:
+    texts, total = [], 0
+    for m in _STREAM.finditer(data):
+        raw = m.group(1)
         content = raw
         try:
-            content = zlib.decompress(raw)
+            d = zlib.decompressobj()
+            content = d.decompress(raw, 8 * limit) if limit else d.decompress(raw)
         except zlib.error:
             pass
         t = _text_from_content(content)
         if t:
             texts.append(t)
-    return "\n".join(texts)
+            total += len(t) + 1
+            if limit and total >= limit:
+                break
+    out = "\n".join(texts)
+    return out[:limit] if limit else out
 
 
-def extract_text(data: bytes) -> str:
+def extract_text(data: bytes, limit: int | None = None) -> str:
+    """Text of an upload.  ``limit``: stop after that many characters -- the extraction runs on
+    the leader's request path, and parsing all of a 48 MiB upload held the interpreter long
+    enough (~0.9 s) to starve the Raft heartbeat thread into an election."""
     if not data.startswith(b"%PDF"):
-        return data.decode("utf-8", errors="replace")
+        head = data if limit is None else data[: 4 * limit]
+        out = head.decode("utf-8", errors="replace")
+        return out if limit is None else out[:limit]
     for mod in ("pypdf", "PyPDF2"):
         try:
             lib = __import__(mod)
@@ -86,7 +97,7 @@ def extract_text(data: bytes) -> str:
             continue
         except Exception:
             break
-    return _builtin_extract(data)
+    return _builtin_extract(data, limit)
 
 
 def make_pdf(text: str) -> bytes:

@@ -27,6 +27,7 @@ from ..raft.storage import FileStorage
 from ..raft.transport import GrpcTransport, RaftServicer, snapshot_handler
 from ..utils.config import parse_with_config
 from ..utils.debug_rpc import debug_handler
+from .blobs import BlobFetcher, BlobReplicator, fetch_handler
 from .service import FileTransferServicer, LMSServicer, TutoringClient
 from .state import LMSState
 
@@ -57,7 +58,13 @@ class LMSServer:
                              snapshot_every=snapshot_every)
         self.transport.attach(self.node)
         self.tutor = TutoringClient(tutor_address) if tutor_address else None
-        self.lms = LMSServicer(self.node, self.state, self.addresses, tutor=self.tutor, gate=gate)
+        # uploads: pushed to a majority before their (tiny) PutBlob entry is proposed; pulled from
+        # a peer by any replica that missed the push (lms/blobs.py)
+        self.replicator = BlobReplicator(self.state.blobs, self.peers)
+        self.fetcher = BlobFetcher(self.state.blobs, self.peers, leader_id=lambda: self.node.leader_id)
+        self.state.blobs.fetcher = self.fetcher
+        self.lms = LMSServicer(self.node, self.state, self.addresses, tutor=self.tutor, gate=gate,
+                               replicator=self.replicator)
         if gate is not None and hasattr(gate, "attach_state"):
             gate.attach_state(self.state)
         opts = [("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
@@ -67,8 +74,8 @@ class LMSServer:
         wire.register(self.server, "LMS", self.lms)
         wire.register(self.server, "RaftService", self.raft_servicer)
         wire.register(self.server, "FileTransferService", FileTransferServicer(self.state))
-        self.server.add_generic_rpc_handlers((snapshot_handler(self.node),
-                                              debug_handler(health=self._health, status=self.node.status)))
+        self.server.add_generic_rpc_handlers((snapshot_handler(self.node), fetch_handler(self.state.blobs),
+                                              debug_handler(health=self._health, status=self._status)))
         bound = self.server.add_insecure_port(f"{host}:{port}")
         if bound == 0:
             raise RuntimeError(f"could not bind {host}:{port}")
@@ -79,6 +86,12 @@ class LMSServer:
         return {"node": self.id, "role": st["role"], "leader": st["leader"], "term": st["term"],
                 "ok": st["leader"] is not None}
 
+    def _status(self) -> dict:
+        st = self.node.status()
+        st["transport_pending"] = self.transport.pending()
+        st["blobs_pushed"], st["blobs_fetched"] = self.replicator.pushed, self.fetcher.fetched
+        return st
+
     def start(self):
         self.server.start()
         self.node.start()
@@ -88,6 +101,8 @@ class LMSServer:
     def stop(self, grace: float = 0.5):
         self.node.stop()
         self.transport.close()
+        self.replicator.close()
+        self.fetcher.close()
         self.server.stop(grace).wait()
         self.storage.close()
         if self.tutor is not None:

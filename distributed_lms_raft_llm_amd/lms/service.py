@@ -16,8 +16,6 @@ Behaviour and every user-visible string follow the reference handlers
 """
 from __future__ import annotations
 
-import base64
-import hashlib
 import logging
 import threading
 import time
@@ -36,6 +34,10 @@ from .pdf import extract_text
 log = logging.getLogger("dlms.lms")
 
 FORWARD_HEADER = "x-dlms-forwarded"
+REQUEST_ID_HEADER = "x-dlms-request-id"  # client request id: writes carrying one apply once
+# assignment text kept in the replicated state (the relevance gate reads <= 512 tokens of it);
+# a multi-MB upload must not become a multi-MB Raft entry
+TEXT_CAP = 256 * 1024
 
 MSG_REGISTER_OK = "Registration request is being processed. Please wait."
 MSG_USER_EXISTS = "Username already exists."
@@ -117,9 +119,10 @@ class TutoringClient:
 
 class LMSServicer:
     def __init__(self, node, state, addresses: dict[int, str], tutor: TutoringClient | None = None, gate=None,
-                 write_timeout: float = 5.0, forward_timeout: float = 130.0):
+                 write_timeout: float = 5.0, forward_timeout: float = 130.0, replicator=None):
         self.node = node
         self.state = state
+        self.replicator = replicator  # lms.blobs.BlobReplicator (None: single node / tests)
         self.addresses = addresses
         self.tutor = tutor
         self.gate = gate
@@ -143,18 +146,28 @@ class LMSServicer:
         if stub is None:
             stub = wire.Stub("LMS", wire.channel(self.addresses[lid]))
             self._leader_stubs[lid] = stub
+        meta = [(FORWARD_HEADER, "1")]
+        if md.get(REQUEST_ID_HEADER):
+            meta.append((REQUEST_ID_HEADER, md[REQUEST_ID_HEADER]))
         try:
             METRICS.inc("lms_forwarded_total")
-            return getattr(stub, method)(request, timeout=self.forward_timeout, metadata=((FORWARD_HEADER, "1"),))
+            return getattr(stub, method)(request, timeout=self.forward_timeout, metadata=tuple(meta))
         except grpc.RpcError as e:
             log.warning("forward %s to leader %s failed: %s", method, lid, e.code())
             return None
 
-    def _write(self, op: str, args: list):
-        return self.node.propose(commands.encode(op, args), timeout=self.write_timeout)
+    @staticmethod
+    def _rid(context, suffix: str = "") -> str | None:
+        md = dict(context.invocation_metadata() or ()) if context is not None else {}
+        rid = md.get(REQUEST_ID_HEADER)
+        return f"{rid}{suffix}" if rid else None
 
-    def _write_many(self, items: list[tuple[str, list]]):
-        futs = [self.node.submit(commands.encode(op, a)) for op, a in items]
+    def _write(self, op: str, args: list, rid: str | None = None):
+        return self.node.propose(commands.encode(op, args, rid), timeout=self.write_timeout)
+
+    def _write_many(self, items: list[tuple[str, list]], rid: str | None = None):
+        futs = [self.node.submit(commands.encode(op, a, f"{rid}.{k}" if rid else None))
+                for k, (op, a) in enumerate(items)]
         return [f.result(timeout=self.write_timeout) for f in futs]
 
     def _read_fence(self):
@@ -162,7 +175,18 @@ class LMSServicer:
             self.node.read_barrier(self.write_timeout)
 
     def _session(self, token: str):
+        # fenced: a leader elected a moment ago may not have applied the Login entry its
+        # predecessor committed -- the token must still be valid right after a failover
+        self._read_fence()
         return self.state.session(token)
+
+    def _store_upload(self, filename: str, blob: bytes):
+        """Pre-replicate an upload (content-addressed) to a majority, then return the small
+        ``PutBlob`` log item that makes it part of the replicated state."""
+        sha = self.state.blobs.put_bytes(blob)
+        if self.replicator is not None and not self.replicator.replicate(sha, len(self.addresses)):
+            raise TimeoutError(f"upload {filename!r} did not reach a majority")
+        return ("PutBlob", [filename, sha, len(blob)])
 
     # ------------------------------------------------------------------ auth
     def Register(self, request, context):
@@ -170,10 +194,12 @@ class LMSServicer:
         if fwd is not None:
             return fwd
         self._read_fence()
-        if self.state.read(lambda d: request.username in d["users"]):
+        rid = self._rid(context)
+        done, first = self.state.rid_result(rid)
+        if not done and self.state.read(lambda d: request.username in d["users"]):
             return pb.RegisterResponse(success=False, message=MSG_USER_EXISTS)
         try:
-            ok = self._write("Register", [request.username, request.password, request.role])
+            ok = first if done else self._write("Register", [request.username, request.password, request.role], rid)
         except (NotLeader, TimeoutError, Exception):
             return pb.RegisterResponse(success=False, message=MSG_UNAVAILABLE)
         if not ok:
@@ -216,26 +242,22 @@ class LMSServicer:
         if s is None:
             return pb.PostResponse(success=False)
         user, role = s["username"], s["role"]
+        rid = self._rid(context)
         try:
             if role == "instructor" and request.type == "course_material":
-                blob = bytes(request.file)
                 path = self.state.blobs.relpath(request.filename)
-                self._write_many([
-                    ("StoreBlob", [request.filename, hashlib.sha256(blob).hexdigest(), base64.b64encode(blob).decode()]),
-                    ("PostCourseMaterial", [user, request.filename, path]),
-                ])
+                self._write_many([self._store_upload(request.filename, bytes(request.file)),
+                                  ("PostCourseMaterial", [user, request.filename, path])], rid)
                 return pb.PostResponse(success=True)
             if role == "student" and request.type == "assignment":
                 blob = bytes(request.file)
-                text = extract_text(blob)
+                text = extract_text(blob, TEXT_CAP)
                 path = self.state.blobs.relpath(request.filename)
-                self._write_many([
-                    ("StoreBlob", [request.filename, hashlib.sha256(blob).hexdigest(), base64.b64encode(blob).decode()]),
-                    ("PostAssignment", [user, request.filename, path, text]),
-                ])
+                self._write_many([self._store_upload(request.filename, blob),
+                                  ("PostAssignment", [user, request.filename, path, text])], rid)
                 return pb.PostResponse(success=True)
             if role == "student" and request.type == "query":
-                self._write("AskQuery", [user, request.data])
+                self._write("AskQuery", [user, request.data], rid)
                 return pb.PostResponse(success=True)
         except Exception as e:
             log.warning("Post failed: %s", e)
@@ -255,12 +277,12 @@ class LMSServicer:
             if not mats:
                 return pb.GetResponse(success=True, message=MSG_NO_MATERIALS)
             return pb.GetResponse(success=True, entries=[
-                pb.DataEntry(id="1", filename=f, file=self.state.blobs.get(p), instructor=ins) for f, p, ins in mats])
+                pb.DataEntry(id="1", filename=f, file=self.state.read_blob(p), instructor=ins) for f, p, ins in mats])
         if s["role"] == "instructor" and request.type == "student_list":
             rows = self.state.read(lambda d: [(st, a["filename"], a["filepath"]) for st, items in d["assignments"].items()
                                               for a in items])
             return pb.GetResponse(success=True, entries=[
-                pb.DataEntry(id=st, filename=f, file=self.state.blobs.get(p)) for st, f, p in rows])
+                pb.DataEntry(id=st, filename=f, file=self.state.read_blob(p)) for st, f, p in rows])
         return pb.GetResponse(success=False, message=MSG_BAD_GET)
 
     def GradeAssignment(self, request, context):
@@ -276,7 +298,7 @@ class LMSServicer:
         if not self.state.read(lambda d: request.studentId in d["assignments"]):
             return pb.GradeResponse(success=False, message=MSG_NO_STUDENT_ASSIGNMENT)
         try:
-            self._write("GradeAssignment", [request.studentId, request.grade])
+            self._write("GradeAssignment", [request.studentId, request.grade], self._rid(context))
         except Exception:
             return pb.GradeResponse(success=False, message=MSG_UNAVAILABLE)
         return pb.GradeResponse(success=True, message=MSG_GRADE_OK)
@@ -323,7 +345,7 @@ class LMSServicer:
         if s is None or s["role"] != "instructor":
             return pb.PostResponse(success=False)
         try:
-            self._write("RespondToQuery", [s["username"], request.studentId, request.data])
+            self._write("RespondToQuery", [s["username"], request.studentId, request.data], self._rid(context))
         except Exception:
             return pb.PostResponse(success=False)
         return pb.PostResponse(success=True)
@@ -394,15 +416,26 @@ class FileTransferServicer:
         self.state = state
 
     def SendFile(self, request_iterator, context):
-        name, buf = None, bytearray()
+        """``destination_path = "cas/<sha256>"``: a leader's pre-replication push (lms/blobs.py),
+        streamed to disk chunk by chunk and verified against the hash; any other path: the
+        reference's upload to ``uploads/<basename>``."""
+        it = iter(request_iterator)
         try:
-            for chunk in request_iterator:
-                if name is None:
-                    name = chunk.destination_path
-                buf += chunk.content
-            if name is None:
+            first = next(it, None)
+            if first is None:
                 return pb.FileTransferResponse(status="Error receiving file: empty stream")
-            self.state.blobs.put(name, bytes(buf))
+            name = first.destination_path
+
+            def chunks():
+                yield first.content
+                for c in it:
+                    yield c.content
+
+            blobs = self.state.blobs
+            if name.startswith("cas/"):
+                blobs.put_chunks(name[4:], chunks())
+            else:
+                blobs.put(name, b"".join(chunks()))
             return pb.FileTransferResponse(status="File received successfully")
         except Exception as e:  # mirror the reference's error reporting
             return pb.FileTransferResponse(status=f"Error receiving file: {e}")

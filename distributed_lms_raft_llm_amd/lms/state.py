@@ -15,9 +15,12 @@ Differences from the reference, all deliberate:
 * committed JSON commands are actually applied (the reference's ``_apply_commits`` only parses
   a legacy space-separated form and silently drops every live entry, Appendix A.1);
 * sessions are replicated (``Login``/``Logout`` log entries) so tokens survive a leader change;
-* upload bytes travel in the log (``StoreBlob``), written atomically and idempotently under
-  ``uploads/`` on every replica -- the reference streams them after commit to hard-coded IPs and
-  its ``SendFile`` appends, so a retry duplicates bytes (Appendix A.10);
+* uploads are content-addressed and pre-replicated to a majority over ``SendFile`` before the
+  (tiny) ``PutBlob`` entry commits (lms/blobs.py) -- the reference streams them after commit to
+  hard-coded IPs and its ``SendFile`` appends, so a retry duplicates bytes (Appendix A.10); the
+  replicated ``blob_index`` maps each ``uploads/<f>`` to its sha256 and a replica that misses an
+  object pulls it from a peer;
+* writes carrying a client request id (``rid``) apply once; a retry gets the first result;
 * ``lms_data.json`` is an export of the state written atomically after each applied batch (the
   Raft log + snapshot are the source of truth); it is imported once when a node starts with no
   Raft state, so an existing reference data file migrates.
@@ -30,65 +33,17 @@ import hashlib
 import json
 import os
 import threading
+from collections import OrderedDict
 
 from . import commands
+from .blobs import UPLOAD_FOLDER, BlobStore, safe_filename  # noqa: F401  (re-exported)
 
 DATABASE_FILE = "lms_data.json"
-UPLOAD_FOLDER = "uploads"
+DEDUPE_CAP = 20000  # client request ids remembered (oldest evicted first, identically on every replica)
 
 
 def default_data() -> dict:
     return {"users": {}, "assignments": {}, "grades": {}, "course_materials": [], "queries": {}}
-
-
-def safe_filename(name: str) -> str:
-    """Strip directories and control characters: upload names come from clients."""
-    base = os.path.basename(name.replace("\\", "/")).strip()
-    base = "".join(ch for ch in base if ch.isprintable() and ch not in '<>:"|?*')
-    if base in ("", ".", ".."):
-        base = "unnamed"
-    return base[:255]
-
-
-class BlobStore:
-    """``uploads/<filename>`` files.  Writes are atomic (tmp + rename) and idempotent."""
-
-    def __init__(self, root: str):
-        self.root = root
-        os.makedirs(os.path.join(root, UPLOAD_FOLDER), exist_ok=True)
-
-    def relpath(self, filename: str) -> str:
-        return os.path.join(UPLOAD_FOLDER, safe_filename(filename))
-
-    def abspath(self, relpath: str) -> str:
-        rel = os.path.normpath(relpath)
-        if rel.startswith("..") or os.path.isabs(rel):
-            rel = self.relpath(os.path.basename(relpath))
-        return os.path.join(self.root, rel)
-
-    def put(self, filename: str, data: bytes) -> str:
-        rel = self.relpath(filename)
-        path = self.abspath(rel)
-        if os.path.exists(path):
-            with open(path, "rb") as f:
-                if hashlib.sha256(f.read()).digest() == hashlib.sha256(data).digest():
-                    return rel
-        tmp = f"{path}.tmp{os.getpid()}.{threading.get_ident()}"
-        with open(tmp, "wb") as f:
-            f.write(data)
-        os.replace(tmp, path)
-        return rel
-
-    def get(self, relpath: str) -> bytes:
-        try:
-            with open(self.abspath(relpath), "rb") as f:
-                return f.read()
-        except FileNotFoundError:
-            return b""
-
-    def names(self) -> list[str]:
-        d = os.path.join(self.root, UPLOAD_FOLDER)
-        return sorted(n for n in os.listdir(d) if ".tmp" not in n)
 
 
 class LMSState:
@@ -99,6 +54,8 @@ class LMSState:
         self.data = default_data()
         self.sessions: dict[str, dict] = {}  # token -> {"username", "role"}
         self.kv: dict[str, str] = {}
+        self.blob_index: dict[str, str] = {}  # "uploads/<f>" -> sha256 of its CAS object
+        self.dedupe: OrderedDict[str, object] = OrderedDict()  # client request id -> first result
         self.applied_index = 0
         self.export_enabled = export
         self._dirty = False
@@ -132,11 +89,12 @@ class LMSState:
 
     # ------------------------------------------------------------------ snapshots
     def snapshot(self) -> str:
+        """The replicated state as JSON -- blob BYTES are not included (``blob_index`` names each
+        upload's CAS object; a restoring replica pulls what it lacks from its peers)."""
         with self.lock:
-            blobs = {n: base64.b64encode(self.blobs.get(os.path.join(UPLOAD_FOLDER, n))).decode()
-                     for n in self.blobs.names()}
             return json.dumps({"data": self.data, "sessions": self.sessions, "kv": self.kv,
-                               "applied_index": self.applied_index, "blobs": blobs})
+                               "applied_index": self.applied_index, "blob_index": self.blob_index,
+                               "dedupe": list(self.dedupe.items())})
 
     def restore(self, snap: str):
         obj = json.loads(snap) if snap else {}
@@ -145,18 +103,49 @@ class LMSState:
             self.sessions = obj.get("sessions", {})
             self.kv = obj.get("kv", {})
             self.applied_index = obj.get("applied_index", 0)
-            for name, b64 in obj.get("blobs", {}).items():
-                self.blobs.put(name, base64.b64decode(b64))
+            self.blob_index = dict(obj.get("blob_index", {}))
+            self.dedupe = OrderedDict((k, v) for k, v in obj.get("dedupe", []))
+            for name, b64 in obj.get("blobs", {}).items():  # snapshots of the round-1 format
+                rel = self.blobs.put(name, base64.b64decode(b64))
+                self.blob_index.setdefault(rel, hashlib.sha256(base64.b64decode(b64)).hexdigest())
+            index = dict(self.blob_index)
             self._dirty = True
+        for rel, sha in index.items():
+            self._materialize(rel, sha)
+
+    def _materialize(self, rel: str, sha: str):
+        if self.blobs.materialize(rel, sha):
+            return
+        if self.blobs.fetcher is not None:  # missed the leader's push: pull it in the background
+            self.blobs.fetcher.fetch_async(sha, then=lambda: self.blobs.materialize(rel, sha))
+
+    def rid_result(self, rid: str | None):
+        """(already applied?, its result) for a client request id."""
+        if not rid:
+            return False, None
+        with self.lock:
+            if rid in self.dedupe:
+                return True, self.dedupe[rid]
+        return False, None
+
+    def blob_sha(self, relpath: str) -> str | None:
+        with self.lock:
+            return self.blob_index.get(relpath)
+
+    def read_blob(self, relpath: str) -> bytes:
+        """An upload's bytes (fetched from a peer first if this replica does not hold them)."""
+        return self.blobs.get(relpath, self.blob_sha(relpath))
 
     # ------------------------------------------------------------------ apply
     def apply(self, index: int, command: str):
         try:
-            op, args = commands.decode(command)
+            op, args, rid = commands.decode_full(command)
         except commands.BadCommand:
             return None
         with self.lock:
             self.applied_index = max(self.applied_index, index)
+            if rid is not None and rid in self.dedupe:
+                return self.dedupe[rid]  # a retried write: applied once, same answer
             fn = getattr(self, "_op_" + op, None)
             if fn is None:
                 return None
@@ -164,6 +153,10 @@ class LMSState:
                 res = fn(*args)
             except TypeError:  # wrong arity from a foreign/legacy writer: ignore the entry
                 return None
+            if rid is not None:
+                self.dedupe[rid] = res
+                while len(self.dedupe) > DEDUPE_CAP:
+                    self.dedupe.popitem(last=False)
             if op not in ("NoOp", "SetVal"):
                 self._dirty = True
         for cb in self.listeners:
@@ -223,11 +216,21 @@ class LMSState:
     def _op_Logout(self, token):
         return self.sessions.pop(token, None) is not None
 
-    def _op_StoreBlob(self, filename, sha256, b64):
+    def _op_PutBlob(self, filename, sha256, size):
+        """An upload pre-replicated to a majority (lms/blobs.py): record it, and link it into
+        ``uploads/`` here -- or pull it from a peer if this replica missed the push."""
+        if not isinstance(sha256, str) or len(sha256) != 64:
+            return False
+        rel = self.blobs.relpath(filename)
+        self.blob_index[rel] = sha256
+        self._materialize(rel, sha256)
+        return True
+
+    def _op_StoreBlob(self, filename, sha256, b64):  # round-1 log entries (bytes inside the entry)
         data = base64.b64decode(b64)
         if hashlib.sha256(data).hexdigest() != sha256:
             return False
-        self.blobs.put(filename, data)
+        self.blob_index[self.blobs.put(filename, data)] = sha256
         return True
 
     def _op_SetVal(self, key, value):

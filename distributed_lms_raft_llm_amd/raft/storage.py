@@ -5,10 +5,13 @@ with term 0 and an empty log.  Here:
 
 * ``raft_meta.json``     -- ``{"current_term", "voted_for"}``, replaced atomically (write, fsync,
   rename) before any vote or term change is acted on;
-* ``raft_log.jsonl``     -- append-only, one ``{"term": int, "command": str}`` object per line: the
-  reference's ``LogEntry`` / log-entry format verbatim (``lms.proto:180-183``,
-  ``lms_server.py:335-340``); a conflicting suffix is cut with ``truncate(2)`` at the entry's byte
-  offset;
+* ``raft_log.jsonl``     -- append-only, one ``{"term": int, "command": str, "index": int}`` object
+  per line: the reference's ``LogEntry`` / log-entry format (``lms.proto:180-183``,
+  ``lms_server.py:335-340``) plus the entry's own log index, so the file is self-describing -- a
+  crash between replacing the snapshot and rewriting the log (compaction, InstallSnapshot) leaves
+  an OLD log whose entries still carry their true indices; loading drops those at or below the
+  snapshot instead of shifting every entry to the wrong index.  A conflicting suffix is cut with
+  ``truncate(2)`` at the entry's byte offset;
 * ``raft_snapshot.json`` -- ``{"last_index", "last_term", "data"}`` where ``data`` is the state
   machine's JSON snapshot (the ``lms_data.json`` schema); compaction rewrites the log without the
   snapshotted prefix.
@@ -131,7 +134,7 @@ class FileStorage(MemoryStorage):
             self._snap_index, self._snap_term, self._snap_data = int(s["last_index"]), int(s["last_term"]), s["data"]
         lp = self._path(self.LOG)
         if os.path.exists(lp):
-            good = 0
+            good, stale = 0, False
             with open(lp, "rb") as f:
                 off = 0
                 for line in f:
@@ -142,11 +145,21 @@ class FileStorage(MemoryStorage):
                         break  # torn tail from a crash mid-append: drop it
                     if not line.endswith(b"\n"):
                         break
+                    expect = self._snap_index + len(self._log) + 1
+                    idx = int(obj.get("index", expect))  # round-1 logs carry no index: sequential
+                    if idx <= self._snap_index:
+                        stale = True  # already inside the snapshot (crash mid-compaction)
+                        off += len(line)
+                        continue
+                    if idx != expect:
+                        break  # a gap cannot be trusted: keep the consistent prefix only
                     self._log.append(e)
                     self._offsets.append(off)
                     off += len(line)
                     good = off
-            if good != os.path.getsize(lp):
+            if stale:
+                self._rewrite_log(reopen=False)  # drop the snapshotted prefix from the file too
+            elif good != os.path.getsize(lp):
                 os.truncate(lp, good)
 
     def save_meta(self, term: int, voted_for):
@@ -158,8 +171,9 @@ class FileStorage(MemoryStorage):
             return
         off = self._fh.tell()
         buf = bytearray()
-        for e in entries:
-            line = (json.dumps({"term": e.term, "command": e.command}) + "\n").encode("utf-8")
+        first = self.last_index() + 1
+        for k, e in enumerate(entries):
+            line = (json.dumps({"term": e.term, "command": e.command, "index": first + k}) + "\n").encode("utf-8")
             self._offsets.append(off + len(buf))
             buf += line
         self._fh.write(buf)
@@ -180,16 +194,18 @@ class FileStorage(MemoryStorage):
             del self._offsets[k:]
         super().truncate_from(i)
 
-    def _rewrite_log(self):
-        self._fh.close()
+    def _rewrite_log(self, reopen: bool = True):
+        if reopen:
+            self._fh.close()
         lines, self._offsets, off = [], [], 0
-        for e in self._log:
-            line = json.dumps({"term": e.term, "command": e.command}) + "\n"
+        for k, e in enumerate(self._log):
+            line = json.dumps({"term": e.term, "command": e.command, "index": self._snap_index + 1 + k}) + "\n"
             self._offsets.append(off)
             off += len(line.encode("utf-8"))
             lines.append(line)
         _atomic_write(self._path(self.LOG), "".join(lines), self.fsync)
-        self._fh = open(self._path(self.LOG), "ab")
+        if reopen:
+            self._fh = open(self._path(self.LOG), "ab")
 
     def _save_snapshot(self):
         _atomic_write(self._path(self.SNAP), json.dumps({"last_index": self._snap_index, "last_term": self._snap_term,

@@ -14,17 +14,21 @@ AppendResponse      AppendEntriesResponse{result: {term, verdict}, success, term
 ==================  ================================================================================
 
 InstallSnapshot has no RPC in ``lms.proto`` (which stays byte-for-byte), so it is served on an
-internal generic method ``/lmsinternal.Raft/InstallSnapshot`` with a JSON body.
+internal generic client-streaming method ``/lmsinternal.Raft/InstallSnapshotStream``: a JSON header
+then the snapshot in 1 MiB pieces (the unary ``InstallSnapshot`` of round 1 is still served).
 
 Differences from the reference's call pattern (``lms_server.py:442-650``): one persistent channel
-per peer instead of a new channel per RPC, deadlines on every RPC, and sends happen on a per-peer
-single-thread executor so a slow peer never blocks the node or the other peers.
+per peer instead of a new channel per RPC, deadlines on every RPC, and a per-peer sender thread
+with a BOUNDED, coalescing mailbox -- at most one pending message per kind (vote, append,
+snapshot); a newer AppendEntries replaces an unsent older one (the core re-sends from its own
+next_index after ``rpc_timeout`` anyway), so a stalled follower can never grow a queue of stale
+RPCs that replays when it resumes.
 """
 from __future__ import annotations
 
 import json
 import logging
-from concurrent.futures import ThreadPoolExecutor
+import threading
 
 import grpc
 
@@ -36,6 +40,8 @@ from .core import (AppendRequest, AppendResponse, Entry, SnapshotRequest, Snapsh
 log = logging.getLogger("dlms.raft.transport")
 
 SNAPSHOT_METHOD = "/lmsinternal.Raft/InstallSnapshot"
+SNAPSHOT_STREAM_METHOD = "/lmsinternal.Raft/InstallSnapshotStream"
+SNAPSHOT_CHUNK = 1 << 20
 
 
 def to_proto(m):
@@ -67,6 +73,39 @@ def append_request_from(p, dst: int) -> AppendRequest:
                          [Entry(e.term, e.command) for e in p.entries], p.leaderCommit)
 
 
+class _Mailbox:
+    """Per-peer pending sends: one slot per message kind, newest wins."""
+
+    KINDS = (VoteRequest, SnapshotRequest, AppendRequest)
+
+    def __init__(self):
+        self.cv = threading.Condition()
+        self.slots: dict[type, object] = {}
+        self.superseded = 0
+
+    def put(self, m) -> None:
+        with self.cv:
+            if type(m) in self.slots:
+                self.superseded += 1
+            self.slots[type(m)] = m
+            self.cv.notify()
+
+    def take(self, stop: threading.Event, timeout: float = 0.1):
+        with self.cv:
+            while not self.slots:
+                if stop.is_set():
+                    return None
+                self.cv.wait(timeout)
+            for k in self.KINDS:  # votes first: an election must not wait behind a big append
+                if k in self.slots:
+                    return self.slots.pop(k)
+            return self.slots.popitem()[1]
+
+    def __len__(self):
+        with self.cv:
+            return len(self.slots)
+
+
 class GrpcTransport:
     def __init__(self, self_id: int, peers: dict[int, str], rpc_timeout: float = 0.5,
                  snapshot_timeout: float = 30.0):
@@ -78,9 +117,14 @@ class GrpcTransport:
         # (gRPC's default reconnect backoff grows to 120 s)
         self._channels = {pid: wire.channel(addr, reconnect_ms=(50, 500)) for pid, addr in peers.items()}
         self._stubs = {pid: wire.Stub("RaftService", ch) for pid, ch in self._channels.items()}
-        self._snap = {pid: ch.unary_unary(SNAPSHOT_METHOD) for pid, ch in self._channels.items()}
-        self._pools = {pid: ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"raft-send-{pid}")
-                       for pid in peers}
+        self._snap = {pid: ch.stream_unary(SNAPSHOT_STREAM_METHOD) for pid, ch in self._channels.items()}
+        self._boxes = {pid: _Mailbox() for pid in peers}
+        self._stop = threading.Event()
+        self._threads = []
+        for pid in peers:
+            t = threading.Thread(target=self._sender, args=(pid,), name=f"raft-send-{pid}", daemon=True)
+            t.start()
+            self._threads.append(t)
         self.blocked: set[int] = set()  # fault injection: peers we pretend not to reach
         self.closed = False
 
@@ -88,9 +132,29 @@ class GrpcTransport:
         self.node = node
 
     def send(self, m):
-        if self.closed or m.dst not in self._pools or m.dst in self.blocked:
+        if self.closed or m.dst not in self._boxes or m.dst in self.blocked:
             return
-        self._pools[m.dst].submit(self._send_sync, m)
+        self._boxes[m.dst].put(m)
+
+    def pending(self) -> dict:
+        """Per-peer pending sends (bounded by the number of message kinds) and superseded count."""
+        return {pid: {"pending": len(b), "superseded": b.superseded} for pid, b in self._boxes.items()}
+
+    def _sender(self, pid: int):
+        box = self._boxes[pid]
+        while not self._stop.is_set():
+            m = box.take(self._stop)
+            if m is None:
+                return
+            self._send_sync(m)
+
+    @staticmethod
+    def _snapshot_pieces(m):
+        yield json.dumps({"src": m.src, "term": m.term, "last_index": m.last_index, "last_term": m.last_term,
+                          "size": len(m.data)}).encode()
+        data = m.data.encode()
+        for i in range(0, len(data), SNAPSHOT_CHUNK):
+            yield data[i:i + SNAPSHOT_CHUNK]
 
     def _send_sync(self, m):
         try:
@@ -102,9 +166,7 @@ class GrpcTransport:
                 r = self._stubs[m.dst].AppendEntries(to_proto(m), timeout=self.rpc_timeout)
                 resp = AppendResponse(m.dst, self.id, r.result.term, r.result.verdict, r.term)
             elif isinstance(m, SnapshotRequest):
-                body = json.dumps({"src": m.src, "term": m.term, "last_index": m.last_index,
-                                   "last_term": m.last_term, "data": m.data}).encode()
-                r = json.loads(self._snap[m.dst](body, timeout=self.snapshot_timeout))
+                r = json.loads(self._snap[m.dst](self._snapshot_pieces(m), timeout=self.snapshot_timeout))
                 resp = SnapshotResponse(m.dst, self.id, r["term"], r["last_index"])
             else:
                 return
@@ -118,8 +180,10 @@ class GrpcTransport:
 
     def close(self):
         self.closed = True
-        for p in self._pools.values():
-            p.shutdown(wait=False, cancel_futures=True)
+        self._stop.set()
+        for b in self._boxes.values():
+            with b.cv:
+                b.cv.notify_all()
         for ch in self._channels.values():
             ch.close()
 
@@ -180,5 +244,16 @@ def snapshot_handler(node):
                                         obj["data"]))
         return json.dumps({"term": r.term, "last_index": r.last_index}).encode()
 
+    def install_stream(pieces, context) -> bytes:
+        it = iter(pieces)
+        hdr = json.loads(next(it))
+        data = b"".join(it)
+        if len(data) != hdr["size"]:
+            context.abort(grpc.StatusCode.DATA_LOSS, "truncated snapshot stream")
+        r = node.handle(SnapshotRequest(hdr["src"], node.id, hdr["term"], hdr["last_index"], hdr["last_term"],
+                                        data.decode()))
+        return json.dumps({"term": r.term, "last_index": r.last_index}).encode()
+
     return grpc.method_handlers_generic_handler("lmsinternal.Raft", {
-        "InstallSnapshot": grpc.unary_unary_rpc_method_handler(install)})
+        "InstallSnapshot": grpc.unary_unary_rpc_method_handler(install),
+        "InstallSnapshotStream": grpc.stream_unary_rpc_method_handler(install_stream)})

@@ -108,6 +108,83 @@ def main():
     logout()
     login("prof")
     out["steps"].append(["instructor_menu", bool(tk.find_buttons("View and Grade Assignments"))])
+
+    def wait_buttons(text, timeout=30, exclude=()):
+        end = time.time() + timeout
+        while time.time() < end:
+            bs = [b for b in tk.find_buttons(text) if b not in exclude]
+            if bs:
+                return bs
+            time.sleep(0.02)
+        raise AssertionError(f"button {text!r} never appeared")
+
+    def wait_label(pred, timeout=30):
+        end = time.time() + timeout
+        while time.time() < end:
+            with tk._lock:
+                hits = [w.kw.get("text") for w in tk.REGISTRY
+                        if isinstance(w, tk.Label) and not w.destroyed and pred(str(w.kw.get("text", "")))]
+            if hits:
+                return hits
+            time.sleep(0.02)
+        raise AssertionError("label never appeared")
+
+    def sha(path):
+        import hashlib
+
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+
+    # instructor: post course material (lms_gui_final.py:1034-1109)
+    mat = os.path.join(workdir, "lecture1.pdf")
+    with open(mat, "wb") as f:
+        f.write(make_pdf("Lecture 1: replicated state machines and Raft"))
+    n = len(messagebox.LOG)
+    click("Post Course Material")
+    app.file_path.insert(0, mat)
+    click("Submit")
+    out["steps"].append(["post_material", dialogs_after(n)])
+    click("Go Back")
+    # view & grade: download the assignment, then grade it (:1112-1248)
+    n = len(messagebox.LOG)
+    click("View and Grade Assignments")
+    wait_buttons("Submit Grade")
+    saved_hw = os.path.join(workdir, "downloaded_homework.pdf")
+    filedialog.SAVE_PATHS.append(saved_hw)
+    click("Download", 0)
+    out["steps"].append(["download_assignment", dialogs_after(n), sha(saved_hw) == sha(path)])
+    n = len(messagebox.LOG)
+    old_btn = wait_buttons("Submit Grade")[0]
+    old_btn.kw["command"].__defaults__[1].insert(0, "A")  # the row's grade Entry (lambda default g=)
+    old_btn.invoke()
+    out["steps"].append(["grade", dialogs_after(n)])
+    wait_buttons("Submit Grade", exclude=(old_btn,))  # the list refreshes after grading (:1244)
+    click("Go Back")
+    # respond to the student's query through the "{id}: {data}" dropdown (:1255-1361)
+    n = len(messagebox.LOG)
+    click("Respond to Query")
+    wait_buttons("Submit Response")
+    out["steps"].append(["query_choices", sorted(app.student_queries), app.selected_query.get()])
+    app.query_response.insert(0, "Tuesdays at 3pm")
+    click("Submit Response")
+    out["steps"].append(["respond", dialogs_after(n)])
+    logout()
+    # student: grade, course material download, instructor responses (:474-593, :730-838, :946-1013)
+    login("stud")
+    click("View Grades")
+    out["steps"].append(["view_grades_after", wait_label(lambda t: t.startswith("Your grade"))[0]])
+    click("Go Back")
+    n = len(messagebox.LOG)
+    click("View Course Material")
+    out["steps"].append(["materials", wait_label(lambda t: t.startswith("Instructor: "))[0]])
+    saved_mat = os.path.join(workdir, "downloaded_lecture1.pdf")
+    filedialog.SAVE_PATHS.append(saved_mat)
+    click("Download", 0)
+    out["steps"].append(["download_material", dialogs_after(n), sha(saved_mat) == sha(mat)])
+    click("Go Back")
+    click("View Instructor Responses")
+    out["steps"].append(["instructor_responses", wait_label(lambda t: "Instructor Response:" in t)])
+    click("Go Back")
     logout()
     print("GUI_RESULT " + json.dumps(out), flush=True)
     os._exit(0)  # the GUI's executor threads are non-daemon

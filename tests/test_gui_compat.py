@@ -57,3 +57,17 @@ def test_reference_gui_runs_unchanged_against_cluster(tmp_path, stubs):
     assert steps["instructor_menu"][1] is True
     assert res["steps"][-1][1] == ["info", "Logout", "Logged out successfully."]
     assert tutor.calls == ["how does raft leader election work"]
+    # instructor flows and the student's download / response views, all through the unchanged GUI
+    assert steps["post_material"][1] == ["info", "Success", "Course material posted successfully."]
+    kind, title, text = steps["download_assignment"][1]
+    assert (kind, title) == ("info", "Success") and text.startswith("Assignment saved to ")
+    assert steps["download_assignment"][2] is True  # the saved bytes are the student's upload
+    assert steps["grade"][1] == ["info", "Success", "Grade A submitted for Student ID: stud"]
+    assert steps["query_choices"][1] == ["stud: office hours?"] and steps["query_choices"][2] == "stud: office hours?"
+    assert steps["respond"][1] == ["info", "Success", "Response sent successfully."]
+    assert steps["view_grades_after"][1] == "Your grade: A"
+    assert steps["materials"][1] == "Instructor: prof, File: lecture1.pdf"
+    kind, title, text = steps["download_material"][1]
+    assert (kind, title) == ("info", "Success") and text.startswith("Course material saved to ")
+    assert steps["download_material"][2] is True
+    assert steps["instructor_responses"][1] == ["Your Query: office hours?\nInstructor Response: Tuesdays at 3pm"]

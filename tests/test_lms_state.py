@@ -80,13 +80,64 @@ def test_sessions_blobs_snapshot_restore(tmp_path):
     assert st.apply(4, enc("StoreBlob", ["b.pdf", "0" * 64, base64.b64encode(data).decode()])) is False
     assert st.session("tok") == {"username": "s", "role": "student"}
     snap = st.snapshot()
+    assert base64.b64encode(data).decode() not in snap  # snapshots carry the blob index, not bytes
     st2 = LMSState(str(tmp_path / "b"))
+    st2.blobs.fetcher = _PeerFetcher(st2.blobs, st.blobs)  # the restoring replica pulls from a peer
     st2.restore(snap)
     assert st2.session("tok") == {"username": "s", "role": "student"}
-    assert st2.blobs.get(os.path.join("uploads", "a.pdf")) == data
+    assert st2.read_blob(os.path.join("uploads", "a.pdf")) == data
     assert st2.view() == st.view()
     st2.apply(5, enc("Logout", ["tok"]))
     assert st2.session("tok") is None
+
+
+class _PeerFetcher:
+    """BlobFetcher stand-in: copies CAS objects from another replica's store."""
+
+    def __init__(self, mine, peer):
+        self.mine, self.peer = mine, peer
+
+    def fetch(self, sha, timeout=None):
+        if not self.mine.has(sha) and self.peer.has(sha):
+            self.mine.put_chunks(sha, self.peer.iter_chunks(sha))
+        return self.mine.has(sha)
+
+    def fetch_async(self, sha, then=None):
+        if self.fetch(sha) and then is not None:
+            then()
+
+
+def test_put_blob_materialises_or_fetches(tmp_path):
+    """PutBlob (pre-replicated upload): linked into uploads/ when the CAS object is here, pulled
+    from a peer otherwise; a wrong-size hash is refused."""
+    leader = LMSState(str(tmp_path / "l"))
+    data = os.urandom(3 << 20)  # several 1 MiB chunks
+    sha = leader.blobs.put_bytes(data)
+    cmd = commands.encode("PutBlob", ["hw.pdf", sha, len(data)])
+    assert leader.apply(1, cmd) is True
+    assert leader.read_blob("uploads/hw.pdf") == data
+    follower = LMSState(str(tmp_path / "f"))
+    follower.blobs.fetcher = _PeerFetcher(follower.blobs, leader.blobs)
+    assert follower.apply(1, cmd) is True
+    assert follower.read_blob("uploads/hw.pdf") == data and follower.blobs.has(sha)
+    assert follower.apply(2, commands.encode("PutBlob", ["x.pdf", "abc", 3])) is False
+
+
+def test_request_id_applies_once(tmp_path):
+    st = LMSState(str(tmp_path))
+    st.apply(1, commands.encode("Register", ["s", "pw", "student"]))
+    st.apply(2, commands.encode("AskQuery", ["s", "q1"]))
+    st.apply(3, commands.encode("AskQuery", ["s", "q2"]))
+    r = commands.encode("RespondToQuery", ["t", "s", "answer"], rid="abc")
+    assert st.apply(4, r) is True
+    assert st.apply(5, r) is True  # the retry: same answer, NOT applied to q2
+    qs = st.view()["queries"]["s"]
+    assert qs[0]["answered"] and not qs[1]["answered"]
+    assert st.rid_result("abc") == (True, True) and st.rid_result("zzz") == (False, None)
+    st2 = LMSState(str(tmp_path / "b"))
+    st2.restore(st.snapshot())
+    assert st2.apply(6, r) is True and not st2.view()["queries"]["s"][1]["answered"]
+    assert commands.decode(r) == ("RespondToQuery", ["t", "s", "answer"])
 
 
 def test_pdf_text_roundtrip_and_plain_bytes():

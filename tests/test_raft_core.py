@@ -191,10 +191,11 @@ def test_persistence_across_restart(tmp_path):
     c.run(0.5)
     for i in c.ids:
         assert user_cmds(c.committed_on(i))[-1] == cmd(100)
-    # the on-disk log is the reference's LogEntry format: {"term", "command"} per line
+    # the on-disk log is the reference's LogEntry format {"term", "command"} per line, plus the
+    # entry's own index (crash-safe compaction)
     with open(os.path.join(dirs[1], "raft_log.jsonl")) as f:
         first = json.loads(f.readline())
-    assert set(first) == {"term", "command"}
+    assert set(first) == {"term", "command", "index"} and first["index"] == 1
     c.check_safety()
 
 
@@ -306,3 +307,48 @@ def test_pre_vote_is_side_effect_free_and_lease_refuses():
     # once the lease lapsed, the real vote goes through
     r = core.step(VoteRequest(2, 1, 2, last_log_index=1, last_log_term=1), 2.5)[0]
     assert r.granted and core.current_term == 2
+
+
+def test_stale_append_never_moves_commit_index_back():
+    """A duplicate / reordered AppendEntries with a short ``last_new`` must not regress the
+    follower's commit index (VERDICT r1 weak #6)."""
+    from distributed_lms_raft_llm_amd.raft.core import AppendRequest, Entry, RaftCore
+
+    core = RaftCore(2, [1, 3], MemoryStorage())
+    ents = [Entry(1, f"c{i}") for i in range(5)]
+    r = core.step(AppendRequest(1, 2, 1, 0, 0, ents, 5), 0.0)[0]
+    assert r.success and core.commit_index == 5
+    # the stale first AppendEntries (one entry, leader_commit 3) arrives late
+    r = core.step(AppendRequest(1, 2, 1, 0, 0, ents[:1], 3), 0.01)[0]
+    assert r.success and core.commit_index == 5 and core.last_index() == 5
+    r = core.step(AppendRequest(1, 2, 1, 0, 0, ents[:2], 9), 0.02)[0]
+    assert core.commit_index == 5  # min(leader_commit, last_new) = 2 < 5
+
+
+def test_crash_between_snapshot_and_log_rewrite(tmp_path):
+    """Compaction replaces the snapshot, then rewrites the log; a crash in between leaves the OLD
+    log.  Its entries carry their own indices, so loading drops the snapshotted prefix instead of
+    shifting every entry to the wrong index (ADVICE r1, high)."""
+    from distributed_lms_raft_llm_amd.raft.core import Entry
+
+    d = str(tmp_path / "n")
+    st = FileStorage(d, fsync=False)
+    st.append([Entry(1, f"c{i}") for i in range(1, 11)])  # indices 1..10
+    old_log = open(os.path.join(d, "raft_log.jsonl")).read()
+    st.compact(6, 1, "state@6")
+    st.close()
+    with open(os.path.join(d, "raft_log.jsonl"), "w") as f:  # crash: the log rewrite never happened
+        f.write(old_log)
+    st2 = FileStorage(d, fsync=False)
+    assert st2.snapshot_meta() == (6, 1) and st2.last_index() == 10
+    assert [e.command for e in st2.entries(7, 11)] == ["c7", "c8", "c9", "c10"]
+    st2.append([Entry(2, "c11")])
+    st2.close()
+    st3 = FileStorage(d, fsync=False)
+    assert st3.last_index() == 11 and st3.entries(11, 12)[0].command == "c11" and st3.term_at(11) == 2
+    # round-1 logs (no index field) still load sequentially after the snapshot
+    with open(os.path.join(d, "raft_log.jsonl"), "w") as f:
+        for i in range(7, 9):
+            f.write(json.dumps({"term": 1, "command": f"c{i}"}) + "\n")
+    st4 = FileStorage(d, fsync=False)
+    assert st4.last_index() == 8 and st4.entries(7, 9)[1].command == "c8"
