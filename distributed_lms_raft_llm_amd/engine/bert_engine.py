@@ -46,27 +46,48 @@ class HipBertEncoder:
                 ln2_g=t(p + "output.LayerNorm.weight"), ln2_b=t(p + "output.LayerNorm.bias"),
             ))
 
+    def _buffers(self, R: int, n: int, S: int):
+        """Activation buffers, grown on demand and reused (no per-call allocator traffic)."""
+        cfg, dev, bf = self.cfg, self.device, torch.bfloat16
+        H, nh = cfg.hidden, cfg.n_head
+        cap = getattr(self, "_cap", (0, 0, 0))
+        if R > cap[0] or n > cap[1] or S > cap[2]:
+            R2, n2, S2 = max(R, cap[0], 256), max(n, cap[1], 8), max(S, cap[2], 64)
+            self._q = torch.empty(R2, H, dtype=bf, device=dev)
+            self._att = torch.empty(R2, H, dtype=bf, device=dev)
+            self._ff = torch.empty(R2, cfg.intermediate, dtype=bf, device=dev)
+            self._kv = torch.empty(2, n2, nh, S2, 64, dtype=bf, device=dev)
+            self._parts = torch.empty(1, R2, H, dtype=torch.float32, device=dev)
+            self._cap = (R2, n2, S2)
+        kc, vc = (self._kv[i].view(-1)[: n * nh * S * 64].view(n, nh, S, 64) for i in (0, 1))  # contiguous
+        return self._q[:R], self._att[:R], self._ff[:R], kc, vc, self._parts[:, :R]
+
     @torch.no_grad()
     def embed(self, batch: list[list[int]]) -> torch.Tensor:
-        """Mean-pooled last hidden state per sequence: f32 [len(batch), H]."""
+        """Mean-pooled last hidden state per sequence: f32 [len(batch), H].  ``batch`` is packed
+        (varlen rows, no padding): the gate encodes every concurrent query in ONE pass."""
+        import numpy as np
+
         cfg, dev = self.cfg, self.device
-        lens = [min(len(ids), cfg.max_position) for ids in batch]
-        R, n, S = sum(lens), len(batch), max(lens)
-        H, nh, eps = cfg.hidden, cfg.n_head, cfg.layer_norm_eps
-        ids = torch.tensor([i for b, L in zip(batch, lens) for i in b[:L]], dtype=torch.int32).to(dev, non_blocking=True)
-        pos = torch.tensor([j for L in lens for j in range(L)], dtype=torch.int32).to(dev, non_blocking=True)
-        seq = torch.tensor([b for b, L in enumerate(lens) for _ in range(L)], dtype=torch.int32).to(dev, non_blocking=True)
-        kvlen = torch.tensor([L for L in lens for _ in range(L)], dtype=torch.int32).to(dev, non_blocking=True)
-        starts = torch.tensor([sum(lens[:b]) for b in range(n)], dtype=torch.int32).to(dev, non_blocking=True)
-        lens_d = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
+        lens_np = np.asarray([max(1, min(len(ids), cfg.max_position)) for ids in batch], dtype=np.int64)
+        lens = lens_np.tolist()
+        R, n, S = int(lens_np.sum()), len(batch), int(lens_np.max())
+        H, eps = cfg.hidden, cfg.layer_norm_eps
+        # every index array in ONE pinned host buffer -> one H2D copy (was six torch.tensor() uploads)
+        ends = np.cumsum(lens_np)
+        starts_np = ends - lens_np
+        host = np.empty(4 * R + 2 * n, dtype=np.int32)
+        host[:R] = np.fromiter((i for b, L in zip(batch, lens) for i in (b[:L] if b else [0])), dtype=np.int64, count=R)
+        host[R:2 * R] = np.arange(R) - np.repeat(starts_np, lens_np)       # positions
+        host[2 * R:3 * R] = np.repeat(np.arange(n), lens_np)              # sequence (cache slot)
+        host[3 * R:4 * R] = np.repeat(lens_np, lens_np)                   # keys seen (bidirectional)
+        host[4 * R:4 * R + n] = starts_np
+        host[4 * R + n:] = lens_np
+        d = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
+        ids, pos, seq, kvlen = d[:R], d[R:2 * R], d[2 * R:3 * R], d[3 * R:4 * R]
+        starts, lens_d = d[4 * R:4 * R + n], d[4 * R + n:]
         x, h = ops.bert_embed_ln(ids, pos, self.word, self.pos, self.type0, self.emb_g, self.emb_b, eps)
-        bf = torch.bfloat16
-        q = torch.empty(R, H, dtype=bf, device=dev)
-        att = torch.empty(R, H, dtype=bf, device=dev)
-        ff = torch.empty(R, cfg.intermediate, dtype=bf, device=dev)
-        kc = torch.empty(n, nh, S, 64, dtype=bf, device=dev)
-        vc = torch.empty_like(kc)
-        parts = torch.empty(1, R, H, dtype=torch.float32, device=dev)
+        q, att, ff, kc, vc, parts = self._buffers(R, n, S)
         tiles = ops.AttnTiles(lens, dev)  # bidirectional: every row of a sequence sees all its keys
         for lw in self.layers:
             ops.gemm(h, lw["w_qkv"], ops.EPI_QKV, bias=lw["b_qkv"], q_out=q, k_cache=kc, v_cache=vc, row_slot=seq,

@@ -751,6 +751,11 @@ class HipGPT2Engine:
             else:
                 self._decode_step(B, repetition_penalty)
 
+    def health_async(self) -> "HostResult | None":
+        """Non-zero ``.result()`` when a TP collective gave up waiting for a peer (the xGMI
+        barrier's error word): the tokens of that chunk are garbage.  None without xGMI."""
+        return self.xgmi.error_async() if self.xgmi is not None else None
+
     def finished_flags(self, B: int) -> list[int]:
         return self.finished[:B].cpu().tolist()
 

@@ -53,6 +53,15 @@ def flags_async(eng, B: int):
     return f(B) if f is not None else _Ready(eng.finished_flags(B))
 
 
+def health_async(eng):
+    f = getattr(eng, "health_async", None)
+    return f() if f is not None else None
+
+
+class PeerStalled(RuntimeError):
+    """A tensor-parallel peer never reached a collective: the affected chunk's tokens are garbage."""
+
+
 def collect_async(eng, slots: list[int]):
     f = getattr(eng, "collect_async", None)
     return f(slots) if f is not None else _Ready(eng.collect(slots))
@@ -173,7 +182,7 @@ class ContinuousBatcher:
                 td = time.perf_counter()
                 with roctx_range("decode_chunk"):
                     eng.decode(B, self.chunk, self.penalty)
-                    cur = (flags_async(eng, B), dict(self._active))
+                    cur = (flags_async(eng, B), dict(self._active), health_async(eng))
                 self.steps += self.chunk
                 TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
                                 steps=self.chunk)
@@ -182,6 +191,10 @@ class ContinuousBatcher:
                 retiring = None
             if prev is not None:  # chunk k's flags while chunk k+1 runs
                 flags = prev[0].result()
+                if prev[2] is not None and prev[2].result():
+                    # fail every live request (the _run handler) rather than return wrong tokens
+                    METRICS.inc(f"{self.name}_peer_stalls")
+                    raise PeerStalled("a tensor-parallel peer timed out in an xGMI collective")
                 # by identity: a slot retired one chunk earlier may already hold a new request
                 done = [s for s, r in prev[1].items() if s < len(flags) and flags[s] and self._active.get(s) is r]
                 if done:

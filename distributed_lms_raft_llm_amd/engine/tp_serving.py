@@ -66,6 +66,11 @@ class TPEngineProxy:
 
         return collect_async(self.engine, slots)
 
+    def health_async(self):  # rank 0's own error word: a peer that stalled breaks its barrier too
+        from .scheduler import health_async
+
+        return health_async(self.engine)
+
     def close(self):
         """Release the followers.  Tolerates followers that are already gone (a launcher that
         signals the whole process group stops them before rank 0 gets here)."""

@@ -7,14 +7,19 @@ What changes (SURVEY.md §7.1 design choice 2): the model is built ONCE per proc
 re-loads it from disk on every query, ~563 ms), runs on the MI355X through the HIP kernels
 (``engine/bert_engine.py``) -- or the torch reference on CPU hosts -- and assignment embeddings are
 computed when the PostAssignment entry is applied and cached, so a query costs one short
-encoder pass.
+encoder pass -- and concurrent queries SHARE that pass: ``check`` hands its query to a small
+batching thread that packs every query waiting within ``window_ms`` (or up to ``max_batch``) into
+one varlen encoder pass (the reference runs a full BERT forward per request, on CPU, after
+re-loading the model).
 """
 from __future__ import annotations
 
 import hashlib
 import logging
 import threading
+import time
 from collections import OrderedDict
+from concurrent.futures import Future
 
 import torch
 
@@ -26,7 +31,8 @@ log = logging.getLogger("dlms.gate")
 
 
 class RelevanceGate:
-    def __init__(self, encoder, tokenizer: BertWordPiece, threshold: float = 0.6, cache_size: int = 4096):
+    def __init__(self, encoder, tokenizer: BertWordPiece, threshold: float = 0.6, cache_size: int = 4096,
+                 window_ms: float = 1.0, max_batch: int = 64):
         self.encoder = encoder
         self.tok = tokenizer
         self.threshold = threshold
@@ -34,6 +40,14 @@ class RelevanceGate:
         self._cache_size = cache_size
         self._lock = threading.Lock()  # one encoder pass at a time (GPU stream / CPU threads)
         self.device = getattr(encoder, "device", torch.device("cpu"))
+        # query batching: concurrent GetLLMAnswer calls share one packed encoder pass
+        self.window_s = window_ms / 1e3
+        self.max_batch = max_batch
+        self._pending: list[tuple[list[int], torch.Tensor, Future]] = []
+        self._pcv = threading.Condition()
+        self._batcher: threading.Thread | None = None
+        self.passes = 0
+        self.batched_queries = 0
 
     @classmethod
     def create(cls, model: str = "bert-base-uncased", device: str = "auto", threshold: float = 0.6,
@@ -79,12 +93,50 @@ class RelevanceGate:
     def warm(self, text: str):
         self._cached(text)
 
+    # ------------------------------------------------------------------ query batching
+    def _score(self, text: str, a: torch.Tensor) -> float:
+        """Cosine(query embedding, ``a``), computed in the next shared batch."""
+        fut: Future = Future()
+        ids = self.tok.encode(text)
+        with self._pcv:
+            if self._batcher is None:
+                self._batcher = threading.Thread(target=self._batch_loop, name="gate-batcher", daemon=True)
+                self._batcher.start()
+            self._pending.append((ids, a, fut))
+            self._pcv.notify()
+        return fut.result()
+
+    def _cosines(self, q: torch.Tensor, a: torch.Tensor) -> list[float]:
+        if hasattr(self.encoder, "cosine"):  # HIP cosine kernel: [n, n], keep the diagonal
+            return torch.diagonal(self.encoder.cosine(q, a)).float().cpu().tolist()
+        return torch.nn.functional.cosine_similarity(q, a, dim=1).tolist()
+
+    def _batch_loop(self):
+        while True:
+            with self._pcv:
+                while not self._pending:
+                    self._pcv.wait()
+                # the first query waits at most window_s for company; a full batch goes at once
+                end = time.monotonic() + self.window_s
+                while len(self._pending) < self.max_batch and time.monotonic() < end:
+                    self._pcv.wait(max(0.0, end - time.monotonic()))
+                batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
+            try:
+                with self._lock, torch.no_grad():
+                    q = self.encoder.embed([ids for ids, _, _ in batch]).float()
+                    a = torch.stack([x.to(q.device, torch.float32) for _, x, _ in batch])
+                    sims = self._cosines(q, a)  # one device->host copy for the whole batch
+                self.passes += 1
+                self.batched_queries += len(batch)
+                for s, (_, _, fut) in zip(sims, batch):
+                    fut.set_result(float(s))
+            except BaseException as e:  # never strand a caller
+                for _, _, fut in batch:
+                    if not fut.done():
+                        fut.set_exception(e)
+
     def similarity(self, query: str, text: str) -> float:
-        q = self.embed([query])[0]
-        a = self._cached(text)
-        if hasattr(self.encoder, "cosine"):
-            return float(self.encoder.cosine(q[None], a[None])[0, 0])
-        return float(torch.nn.functional.cosine_similarity(q[None], a[None]).item())
+        return self._score(query, self._cached(text))
 
     def check(self, query: str, assignment_text: str) -> tuple[bool, float]:
         s = self.similarity(query, assignment_text)

@@ -145,6 +145,7 @@ def _bind(L):
                        "dlms_xgmi_free": [P], "dlms_ipc_get_handle": [P, P],
                        "dlms_ipc_open": [P, ctypes.POINTER(ctypes.c_void_p)], "dlms_ipc_close": [P],
                        "dlms_xgmi_error": [P, I, ctypes.POINTER(ctypes.c_uint)],
+                       "dlms_xgmi_error_async": [P, P, P],
                        "dlms_xgmi_allreduce_f32": [ctypes.POINTER(XgmiArgs), P],
                        "dlms_xgmi_allgather_u64": [ctypes.POINTER(XgmiArgs), P]}.items():
         fn = getattr(L, name)

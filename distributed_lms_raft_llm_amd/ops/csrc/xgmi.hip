@@ -229,6 +229,13 @@ extern "C" int dlms_xgmi_error(void* base, int clear, unsigned* out) {
     return (int)hipMemset(e, 0, sizeof(unsigned));
 }
 
+// The error word copied to (pinned) host memory behind the work already on ``stream`` -- the
+// serving loop polls it once per decode chunk without a device-wide synchronise.
+extern "C" int dlms_xgmi_error_async(void* base, unsigned* dst, hipStream_t stream) {
+    unsigned* e = reinterpret_cast<unsigned*>(base) + XGMI_ERR_WORD;
+    return (int)hipMemcpyAsync(dst, e, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
+}
+
 extern "C" int dlms_xgmi_allreduce_f32(const XgmiArgs* a, hipStream_t stream) {
     if (int r = xgmi_check(a, a->n * 4)) return r;
     if (a->n % 4) return (int)hipErrorInvalidValue;

@@ -99,6 +99,16 @@ class XgmiComm:
             ops._check(ops.lib().dlms_xgmi_error(self._base, int(clear), ctypes.byref(v)), "dlms_xgmi_error")
         return v.value
 
+    def error_async(self):
+        """The error word as a copy in flight (pinned host memory, enqueued on the current stream
+        behind the work issued so far); ``.result()`` waits for that copy only."""
+        from ..engine.gpt2_engine import HostResult
+
+        t = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        ops._check(ops.lib().dlms_xgmi_error_async(self._base, ctypes.c_void_p(t.data_ptr()), ops._stream()),
+                   "dlms_xgmi_error_async")
+        return HostResult(lambda: int(t[0]), keep=(t,))
+
     def check(self):
         if self.error():
             raise RuntimeError("xGMI collective: a peer never reached the barrier (timed out)")

@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running (multi-process clusters)")
+    config.addinivalue_line("markers", "multigpu(n): needs n GPUs of one node (skipped when fewer are visible)")
 
 
 def pytest_collection_modifyitems(config, items):
@@ -21,6 +22,11 @@ def pytest_collection_modifyitems(config, items):
     except Exception:  # pragma: no cover
         has_gpu = False
     if has_gpu:
+        ngpu = torch.cuda.device_count()
+        for item in items:
+            m = item.get_closest_marker("multigpu")
+            if m is not None and ngpu < (m.args[0] if m.args else 2):
+                item.add_marker(pytest.mark.skip(reason=f"needs {m.args[0] if m.args else 2} GPUs, {ngpu} visible"))
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")
     for item in items:

@@ -56,7 +56,9 @@ class KeywordGate:
 
 
 class Cluster:
-    def __init__(self, n: int, tmp_path, tutor_address=None, gate=None, fsync=False, snapshot_every: int = 2000):
+    def __init__(self, n: int, tmp_path, tutor_address=None, gate=None, fsync=False, snapshot_every: int = 2000,
+                 raft_config: RaftConfig | None = None):
+        self.raft_config = raft_config
         self.ports = free_ports(n)
         self.addrs = {i + 1: f"127.0.0.1:{p}" for i, p in enumerate(self.ports)}
         self.tmp = tmp_path
@@ -72,7 +74,7 @@ class Cluster:
         peers = {j: a for j, a in self.addrs.items() if j != i}
         srv = LMSServer(i, self.ports[i - 1], peers, str(self.tmp / f"node{i}"), host="127.0.0.1",
                         advertise=self.addrs[i], tutor_address=self.tutor_address, gate=self.gate,
-                        raft_config=RaftConfig(), fsync=self.fsync, workers=16,
+                        raft_config=self.raft_config or RaftConfig(), fsync=self.fsync, workers=16,
                         snapshot_every=self.snapshot_every)
         self.servers[i] = srv.start()
         return srv

@@ -68,3 +68,66 @@ def test_hip_encoder_matches_reference(name):
         torch.testing.assert_close(got[b], ref[b], atol=5e-2, rtol=5e-2)
     sim = enc.cosine(got_d, got_d).cpu()
     torch.testing.assert_close(torch.diagonal(sim), torch.ones(len(batch)), atol=1e-5, rtol=1e-5)
+
+
+def test_gate_batches_concurrent_queries_cpu():
+    """concurrent checks share packed encoder passes and score exactly like serial
+    single-query passes."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from distributed_lms_raft_llm_amd.gate.relevance import RelevanceGate
+
+    gate = RelevanceGate.create("bert-tiny", device="cpu", threshold=0.6)
+    gate.window_s = 0.02
+    text = "raft replicates a log of commands across a majority of nodes"
+    queries = [f"question {k} about " + " ".join(["leader", "term", "vote", "log"][: 1 + k % 4]) for k in range(24)]
+    ref = []
+    for qtext in queries:  # serial oracle: one encoder pass per query, no batcher
+        q = gate.embed([qtext])[0]
+        a = gate.embed([text])[0]
+        ref.append(torch.nn.functional.cosine_similarity(q[None], a[None]).item())
+    with ThreadPoolExecutor(24) as ex:
+        got = list(ex.map(lambda qt: gate.check(qt, text)[1], queries))
+    for g_, r_ in zip(got, ref):
+        assert abs(g_ - r_) < 1e-5
+    assert gate.batched_queries == len(queries)
+    assert gate.passes < len(queries)  # at least some queries shared a pass
+
+
+@pytest.mark.gpu
+def test_hip_gate_batched_at_512_tokens():
+    """Packed varlen passes at the reference's 512-token truncation: every row of a mixed batch
+    (1..512 tokens) matches the fp32 torch reference, and the gate's batched scores match it."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from distributed_lms_raft_llm_amd.engine.bert_engine import HipBertEncoder
+    from distributed_lms_raft_llm_amd.gate.relevance import RelevanceGate
+
+    cfg, w = _weights("bert-base-uncased")
+    for k, v in w.items():
+        if v.dim() == 2 and "embeddings" not in k:
+            w[k] = v.to(torch.bfloat16).float()
+    enc = HipBertEncoder(cfg, w)
+    g = torch.Generator().manual_seed(1)
+    lens = [512, 1, 37, 512, 300, 128, 511, 2]
+    batch = [torch.randint(110, cfg.vocab_size, (L,), generator=g).tolist() for L in lens]
+    got = enc.embed(batch).float().cpu()
+    ref = BertReference(cfg, w, device="cuda").embed(batch).cpu()
+    for b in range(len(batch)):
+        cos = torch.nn.functional.cosine_similarity(got[b], ref[b], dim=0).item()
+        assert cos > 0.999, (lens[b], cos)
+    # through the gate's batcher, 32 concurrent queries against one assignment text
+    from distributed_lms_raft_llm_amd.tokenizer import BertWordPiece
+
+    gate = RelevanceGate(enc, BertWordPiece(None, vocab_size=cfg.vocab_size, max_length=cfg.max_position), 0.6)
+    gate.window_s = 0.005
+    text = " ".join(f"w{k}" for k in range(600))  # truncated at 512 tokens
+    queries = [" ".join(f"w{j}" for j in range(k, k + 5 + 13 * k)) for k in range(32)]
+    with ThreadPoolExecutor(32) as ex:
+        got_s = list(ex.map(lambda q: gate.check(q, text)[1], queries))
+    a = enc.embed([gate.tok.encode(text)]).float()
+    for q, s in zip(queries, got_s):
+        qe = enc.embed([gate.tok.encode(q)]).float()
+        r = torch.nn.functional.cosine_similarity(qe, a).item()
+        assert abs(s - r) < 2e-3, (q[:20], s, r)
+    assert gate.passes < len(queries)

@@ -187,3 +187,33 @@ def test_pipelined_loop_readmits_retired_slots_immediately(engine_cls):
         cb.stop()
     assert outs == [solo(p, 12) for p in prompts]
     assert cb.completed == 30 and eng.admitted_while_busy > 0
+
+
+def test_stalled_tp_peer_fails_requests_instead_of_returning_garbage():
+    """The xGMI barrier's error word is polled once per chunk (``health_async``): when a TP peer
+    timed out, every live request fails loudly and the batcher refuses new work."""
+    from distributed_lms_raft_llm_amd.engine.scheduler import PeerStalled
+
+    class StallingEngine(FakeSlotEngine):
+        def __init__(self):
+            super().__init__(max_batch=2, max_length=10 ** 6)
+            self.stop_at_eos = False
+            self.chunks = 0
+
+        def decode(self, B, steps, penalty):
+            super().decode(B, steps, penalty)
+            self.chunks += 1
+
+        def health_async(self):
+            word = 1 if self.chunks >= 3 else 0  # a peer stalls during the third chunk
+            return SimpleNamespace(result=lambda: word)
+
+    eng = StallingEngine()
+    cb = ContinuousBatcher(eng, chunk=2)
+    f = cb.submit([1, 2, 3])
+    with pytest.raises(PeerStalled):
+        f.result(10)
+    time.sleep(0.05)
+    with pytest.raises(RuntimeError):
+        cb.submit([4])
+    cb.stop()
