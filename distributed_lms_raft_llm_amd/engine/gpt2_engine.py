@@ -210,6 +210,7 @@ class HipGPT2Engine:
         # per (row, head) pair, the default: 256/512/1024 blocks measured -6 % / +0.3 % / +1 %, i.e.
         # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
         self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "0"))
+        self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
         if self.overlap_parts not in (2, 3, 4):
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
         if latency_path is None:
@@ -226,7 +227,9 @@ class HipGPT2Engine:
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
         self.lm_head_sh = None
-        if not self.w.fp8 and self.max_batch >= self.PS_LM_MIN_ROWS and os.environ.get("DLMS_PS_LMHEAD", "1") != "0":
+        ps_lm = self.max_batch >= self.PS_LM_MIN_ROWS and os.environ.get("DLMS_PS_LMHEAD", "1") != "0"
+        if not self.w.fp8 and (ps_lm or (self.small_max > 0 and self.lm_skinny)):
+            # (the latency path's skinny LM head reads the same pre-shuffled copy)
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
@@ -255,6 +258,8 @@ class HipGPT2Engine:
         self.x = torch.zeros(B, D, dtype=f32, device=dev)
         # second residual buffer: the latency path's fused add+LN kernels advance x by ping-pong
         self.x2 = torch.zeros(min(B, 64), D, dtype=f32, device=dev)
+        # cross-workgroup split attention (few rows, long caches): partials + arrival counters
+        self.attn_ws = ops.AttnSplitWorkspace(self.SPLIT_ATTN_MAX_PAIRS, 2, dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
         self.h = torch.zeros(B, D, dtype=bf, device=dev)
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
@@ -378,8 +383,9 @@ class HipGPT2Engine:
             ops.tile_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, r.tiles, out=r.att)
         elif r.M * self.w.n_heads_local <= self.SPLIT_ATTN_MAX_PAIRS:
             # decode with few (row, head) pairs: split-K flash-decode puts NW waves on each pair's keys
+            nw, ns = ops.attention_split_geometry(r.M * self.w.n_heads_local, self.max_length)
             ops.attention_split(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
-                                waves=ops.attention_split_waves(self.max_length))
+                                waves=nw, splits=ns, workspace=self.attn_ws)
         elif r.persist_attn:
             # overlapped step: a fixed low-occupancy grid leaves wave slots to the other half's GEMMs
             ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
@@ -431,10 +437,15 @@ class HipGPT2Engine:
         hi = lo + B
         seen_rows = self.seen[lo:hi] if seen is None else seen
         P = self.key_parts.shape[1]  # partial keys per row the LM head writes (and the consumer reads)
-        if hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B >= self.PS_LM_MIN_ROWS:
+        if hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B >= self.PS_LM_MIN_ROWS and \
+                self.max_batch >= self.PS_LM_MIN_ROWS:
             P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16)
             ops.gemm_ps(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                         vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
+        elif hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B <= self.small_max and self.lm_skinny:
+            # latency path: pre-shuffled skinny MFMA LM head (non-temporal weight stream)
+            ops.skinny_gemm(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi],
+                            seen=seen_rows, vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
         elif hidden.dtype == ops.FP8:
             ops.gemm(hidden, self.w.lm_head8, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                      vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty, a_scale=hscale,

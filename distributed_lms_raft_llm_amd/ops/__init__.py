@@ -129,7 +129,7 @@ def _bind(L):
         "dlms_mean_pool": [P, P, P, P, I, I, P],
         "dlms_cosine": [P, P, P, I, I, I, F, P],
         "dlms_skinny_gemm": [I, P, I, P, P, F, P, I, I, I, ctypes.POINTER(GemmEpi), P],
-        "dlms_attention_split": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, P],
+        "dlms_attention_split": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, I, P, P, I, P],
         "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
                                    ctypes.POINTER(GemmEpi), P],
         "dlms_skinny_addln_max_rows": [I],
@@ -871,11 +871,42 @@ def attention_split_waves(kv_len_max: int) -> int:
     return 16
 
 
+ATTN_WS_STRIDE = 68  # floats per cross-workgroup partial (skinny.hip)
+ATTN_SPLIT_SYNC = int(os.environ.get("DLMS_ATTN_SPLIT_SYNC", "2"))
+
+
+def attention_split_geometry(pairs: int, kv_len_max: int, cus: int = 256) -> tuple[int, int]:
+    """(waves, workgroups) per (row, head) for ``attention_split``.  Splitting a pair's keys over
+    several workgroups fills more CUs but adds two dependent global round trips (arrival atomic,
+    partial reload) to the kernel's latency chain; measured on MI355X (profiles/r2_attn_splitwg.jsonl)
+    that only pays for a handful of pairs with long caches (B=1, T=1024: 9.8 vs 11.1 us), and is
+    neutral to slower from B=8 on -- there, one 16-wave workgroup per pair is kept."""
+    nw = attention_split_waves(kv_len_max)
+    if pairs <= 32 and kv_len_max > 512:
+        return 8, 4
+    return nw, 1
+
+
+class AttnSplitWorkspace:
+    """Partials + arrival counters for cross-workgroup ``attention_split`` (counters start at 0
+    and every launch re-arms them, so one workspace serves every replay of a captured graph)."""
+
+    def __init__(self, pairs: int, splits: int, device):
+        self.pairs, self.splits = pairs, splits
+        self.partials = torch.empty(pairs * splits * ATTN_WS_STRIDE, dtype=torch.float32, device=device)
+        self.counters = torch.zeros(pairs, dtype=torch.int32, device=device)
+
+    def fits(self, pairs: int, splits: int) -> bool:
+        return pairs <= self.pairs and pairs * splits <= self.pairs * self.splits
+
+
 def attention_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
                     row_kvlen: torch.Tensor, out: torch.Tensor | None = None, scale: float | None = None,
-                    waves: int = 16):
-    """Split-K flash-decode: one workgroup of ``waves`` waves per (row, head), each streaming a
-    slice of the keys, merged by log-sum-exp.  Same contract as ``row_attention``."""
+                    waves: int = 16, splits: int = 1, workspace: "AttnSplitWorkspace | None" = None,
+                    sync: int | None = None):
+    """Split-K flash-decode: ``splits`` workgroups of ``waves`` waves per (row, head), each wave
+    streaming a slice of the keys; waves merge by log-sum-exp in LDS, workgroups through a
+    workspace merged by the last to arrive.  Same contract as ``row_attention``."""
     _req(q, torch.bfloat16, "q", 2)
     _req(k_cache, torch.bfloat16, "k_cache", 4)
     _req(v_cache, torch.bfloat16, "v_cache", 4)
@@ -889,12 +920,22 @@ def attention_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         raise ValueError("attention_split: index arrays too short")
     if waves not in (2, 4, 8, 16):
         raise ValueError("attention_split: waves in {2, 4, 8, 16}")
+    if not 1 <= splits <= 64:
+        raise ValueError("attention_split: splits in [1, 64]")
     if out is None:
         out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=q.device)
     _req(out, torch.bfloat16, "out", 2)
+    ws_p = cnt_p = None
+    if splits > 1:
+        if workspace is None:
+            workspace = AttnSplitWorkspace(R * H, splits, q.device)
+        if not workspace.fits(R * H, splits):
+            raise ValueError("attention_split: workspace too small")
+        ws_p, cnt_p = _p(workspace.partials), _p(workspace.counters)
     sc = (1.0 / 8.0) if scale is None else scale
     _check(lib().dlms_attention_split(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen),
-                                      _p(out), out.stride(0), R, H, T, S, float(sc), int(waves), _stream()),
+                                      _p(out), out.stride(0), R, H, T, S, float(sc), int(waves), int(splits),
+                                      ws_p, cnt_p, ATTN_SPLIT_SYNC if sync is None else int(sync), _stream()),
            "attention_split")
     return out
 

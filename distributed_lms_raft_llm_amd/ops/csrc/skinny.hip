@@ -20,6 +20,8 @@
 // EPI_F32 (x += acc + bias, in place) / EPI_PARTIAL (TP: raw partial for the all-reduce) /
 // EPI_ARGMAX (repetition penalty + per-row argmax key per 64 columns, the LM-head layout of gemm.hip).
 #include "common.h"
+#include <type_traits>
+#include <stdlib.h>
 
 enum { SK_BF16 = 0, SK_GELU_TANH = 1, SK_F32 = 3, SK_QKV = 4, SK_ARGMAX = 5, SK_PARTIAL = 6 };
 
@@ -37,6 +39,18 @@ __device__ __forceinline__ bf16x8_t load_wfrag(const bf16x8_t* p) {
 #else
     return *p;
 #endif
+}
+
+// The batch-1 LM head streams 77 MB once per token: non-temporal loads keep it from evicting the
+// 12 layers' ~170 MB of weights out of the 256 MiB Infinity Cache (a cyclic 248 MB stream through
+// an LRU cache of about that size would otherwise miss on every layer).  DLMS_LM_NT=0 turns it off.
+static int lm_head_nt() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DLMS_LM_NT");
+        v = (e == nullptr || e[0] != '0') ? 1 : 0;
+    }
+    return v;
 }
 
 // A fragment of rows [16 mt, 16 mt + 16) at k-block kb from the LDS LayerNorm image
@@ -139,7 +153,7 @@ template <int EPI, bool LN, int MT, int NW, int CG, int KBW>
 __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const void* __restrict__ A, int lda,
                                                             const float* __restrict__ ln_g, const float* __restrict__ ln_b,
                                                             float eps, const bf16_t* __restrict__ Wsh, int M, int N,
-                                                            int K, GemmEpi ep) {
+                                                            int K, GemmEpi ep, int wnt) {
     constexpr int WPG = NW / CG;
     static_assert(NW % CG == 0, "whole waves per column group");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -160,7 +174,10 @@ __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const void* __rest
     const int last = nk > 0 ? nk - 1 : 0;
     bf16x8_t b[KBW];
 #pragma unroll
-    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
+    for (int u = 0; u < KBW; ++u) {
+        const bf16x8_t* p = wsrc + (size_t)(u < nk ? u : last) * 64;
+        b[u] = wnt ? __builtin_nontemporal_load(p) : load_wfrag(p);
+    }
     bf16x8_t a[LN ? 1 : KBW][MT];
     if constexpr (!LN) {
 #pragma unroll
@@ -270,8 +287,9 @@ static hipError_t launch_skinny(const void* A, int lda, const float* g, const fl
         if (e != hipSuccess) return e;
         attr_set = true;
     }
+    const int wnt = EPI == SK_ARGMAX ? lm_head_nt() : 0;
     hipLaunchKernelGGL((skinny_gemm_kernel<EPI, LN, MT, NW, CG, KBW>), dim3(N / (16 * CG)), dim3(64 * NW), lds, stream,
-                       A, lda, g, b, eps, W, M, N, K, ep);
+                       A, lda, g, b, eps, W, M, N, K, ep, wnt);
     return hipGetLastError();
 }
 
@@ -549,25 +567,33 @@ extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const float* x_in, float* 
 // lane&7) owns dims [8c, 8c+8) of keys 8i + g), then a log-sum-exp merge of the NW partial
 // (max, sum, acc[64]) triples in a fixed order through LDS.  At batch 1 and 1024 cached keys this
 // puts 12 x NW waves on the KV stream instead of 12.
-template <int NW>
+constexpr int ATTN_WS_STRIDE = 68;  // floats per partial: m, l, pad, pad, o[64] (16-byte aligned o)
+
+template <int NW, int SYNC>
 __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __restrict__ q, int ldq,
                                                            const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                                            const int* __restrict__ row_slot,
                                                            const int* __restrict__ row_kvlen, bf16_t* out, int ldo,
-                                                           int H, int t_max, int n_slots, float scale_log2) {
+                                                           int H, int t_max, int n_slots, float scale_log2,
+                                                           float* __restrict__ ws, int* __restrict__ cnt, int NS) {
     __shared__ float part[NW][8][10];  // per wave, per dim chunk c: m, l, acc[8]
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = blockIdx.x;
     const int r = blockIdx.y;
+    const int sw = blockIdx.z;  // which of the NS workgroups of this (row, head)
     const int g = lane >> 3;
     const int c = lane & 7;
     const int slot = (int)dlms_idx(row_slot[r], n_slots, CHK_ATTN_SLOT);
     int kvlen = row_kvlen[r];
     kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
-    const int span = ((kvlen + NW - 1) / NW + 7) & ~7;
-    const int t_lo = wave * span;
-    const int t_hi = t_lo + span < kvlen ? t_lo + span : kvlen;
+    // keys [w_lo, w_hi) belong to this workgroup, then split evenly over its NW waves
+    const int wspan = ((kvlen + NS - 1) / NS + 7) & ~7;
+    const int w_lo = sw * wspan < kvlen ? sw * wspan : kvlen;
+    const int w_hi = w_lo + wspan < kvlen ? w_lo + wspan : kvlen;
+    const int span = ((w_hi - w_lo + NW - 1) / NW + 7) & ~7;
+    const int t_lo = w_lo + wave * span < w_hi ? w_lo + wave * span : w_hi;
+    const int t_hi = t_lo + span < w_hi ? t_lo + span : w_hi;
     const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
     const bf16_t* K = kc + head_off + c * 8;
     const bf16_t* V = vc + head_off + c * 8;
@@ -637,7 +663,8 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
         for (int j = 0; j < 8; ++j) part[wave][c][2 + j] = acc[j];
     }
     __syncthreads();
-    if (wave == 0 && g == 0) {
+    if (wave != 0) return;
+    if (g == 0) {
         float M_ = -INFINITY;
 #pragma unroll
         for (int w = 0; w < NW; ++w) M_ = fmaxf(M_, part[w][c][0]);
@@ -651,30 +678,90 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
 #pragma unroll
             for (int j = 0; j < 8; ++j) o8[j] += part[w][c][2 + j] * f;
         }
-        const float inv = 1.f / L;
+        if (NS == 1) {
+            const float inv = 1.f / L;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o8[j] *= inv;
-        *reinterpret_cast<uint4*>(out + (size_t)r * ldo + h * 64 + c * 8) = pack8(o8);
+            for (int j = 0; j < 8; ++j) o8[j] *= inv;
+            *reinterpret_cast<uint4*>(out + (size_t)r * ldo + h * 64 + c * 8) = pack8(o8);
+            return;
+        }
+        // several workgroups per (row, head): publish (m, l, unnormalised o[64])
+        float* my = ws + ((size_t)(r * H + h) * NS + sw) * ATTN_WS_STRIDE;
+        if (SYNC == 0) {
+            if (c == 0) {
+                my[0] = M_;
+                my[1] = L;
+            }
+            *reinterpret_cast<float4*>(my + 4 + c * 8) = make_float4(o8[0], o8[1], o8[2], o8[3]);
+            *reinterpret_cast<float4*>(my + 8 + c * 8) = make_float4(o8[4], o8[5], o8[6], o8[7]);
+        } else {  // device-coherent (write-through) stores: nothing dirty is left in this XCD's L2
+            if (c == 0) {
+                __hip_atomic_store(my, M_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(my + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                __hip_atomic_store(my + 4 + c * 8 + j, o8[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
+    if (NS == 1) return;
+    // last-arriver merge (stream-K fix-up): publish our partial device-wide, count arrivals;
+    // the workgroup that arrives last merges all NS partials and re-arms the counter.  Nobody
+    // waits on anybody, so there is no co-residency assumption.
+    if (SYNC == 2)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // our coherent stores are complete
+    else
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    int old = 0;
+    if (lane == 0) old = atomicAdd(cnt + r * H + h, 1);
+    old = __shfl(old, 0, 64);
+    if (old != NS - 1) return;
+    if (SYNC != 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const float* base = ws + (size_t)(r * H + h) * NS * ATTN_WS_STRIDE;
+    auto ld = [](const float* p) {
+        return SYNC == 0 ? *p : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    float M_ = -INFINITY;
+    for (int k = 0; k < NS; ++k) M_ = fmaxf(M_, ld(base + k * ATTN_WS_STRIDE));
+    float L = 0.f, o = 0.f;
+    for (int k = 0; k < NS; ++k) {
+        const float* pk = base + k * ATTN_WS_STRIDE;
+        const float mk = ld(pk);
+        if (mk == -INFINITY) continue;
+        const float f = exp2f(mk - M_);
+        L += ld(pk + 1) * f;
+        o += ld(pk + 4 + lane) * f;
+    }
+    out[(size_t)r * ldo + h * 64 + lane] = f32_to_bf16(o / L);
+    if (lane == 0) atomicExch(cnt + r * H + h, 0);
 }
 
 extern "C" hipError_t dlms_attention_split(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                            const int* row_kvlen, void* out, int ldo, int R, int H, int t_max,
-                                           int n_slots, float scale, int nw, hipStream_t stream) {
-    if (R <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
+                                           int n_slots, float scale, int nw, int ns, float* ws, int* cnt,
+                                           int sync, hipStream_t stream) {
+    if (R <= 0 || H <= 0 || t_max <= 0 || ns < 1 || ns > 64) return hipErrorInvalidValue;
+    if (ns > 1 && (ws == nullptr || cnt == nullptr)) return hipErrorInvalidValue;
     const float sl2 = scale * 1.4426950408889634f;
     auto go = [&](auto kern, int threads) {
-        hipLaunchKernelGGL(kern, dim3(H, R), dim3(threads), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
+        hipLaunchKernelGGL(kern, dim3(H, R, ns), dim3(threads), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
                            reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
-                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, n_slots, sl2);
+                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, n_slots, sl2, ws, cnt, ns);
     };
-    switch (nw) {
-        case 2: go(attn_split_kernel<2>, 128); break;
-        case 4: go(attn_split_kernel<4>, 256); break;
-        case 8: go(attn_split_kernel<8>, 512); break;
-        case 16: go(attn_split_kernel<16>, 1024); break;
-        default: return hipErrorInvalidValue;
-    }
+    auto pick = [&](auto sync_c) -> bool {
+        constexpr int S = decltype(sync_c)::value;
+        switch (nw) {
+            case 2: go(attn_split_kernel<2, S>, 128); return true;
+            case 4: go(attn_split_kernel<4, S>, 256); return true;
+            case 8: go(attn_split_kernel<8, S>, 512); return true;
+            case 16: go(attn_split_kernel<16, S>, 1024); return true;
+            default: return false;
+        }
+    };
+    bool ok = sync == 0 ? pick(std::integral_constant<int, 0>{})
+            : sync == 1 ? pick(std::integral_constant<int, 1>{})
+                        : pick(std::integral_constant<int, 2>{});
+    if (!ok) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -46,6 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--batches", default="1,4,16,32")
+    ap.add_argument("--attn-only", action="store_true")
     ap.add_argument("--cold-mb", type=int, default=512)
     ap.add_argument("--T", default="150,1024")
     args = ap.parse_args()
@@ -53,7 +54,7 @@ def main():
     D = args.d
     shapes = {"qkv": (3 * D, D), "oproj": (D, D), "fc": (4 * D, D), "proj": (D, 4 * D), "lmhead": (50304, D)}
     for M in [int(m) for m in args.batches.split(",")]:
-        for op, (N, K) in shapes.items():
+        for op, (N, K) in ({} if args.attn_only else shapes).items():
             copies = max(1, min(24, args.cold_mb * (1 << 20) // (N * K * 2)))
             ws = [torch.randn(N, K, device=dev).mul_(0.02).to(torch.bfloat16) for _ in range(copies)]
             wsh = [ops.shuffle_weight(w) for w in ws]
@@ -105,6 +106,13 @@ def main():
             for nw in (4, 8, 16):
                 res[f"split{nw}"] = graph_time(lambda i: ops.attention_split(q, *caches[i % nrot], slot, kvlen, out=out,
                                                                              waves=nw))
+            geo = ops.attention_split_geometry(M * H, T)
+            wsp = ops.AttnSplitWorkspace(M * H, 64, dev)
+            for nw, ns in sorted({(4, 2), (4, 4), (4, 8), (2, 8), (8, 4), (4, 16), geo}):
+                if ns > 1:
+                    res[f"splitwg{nw}x{ns}" + ("*" if (nw, ns) == geo else "")] = graph_time(
+                        lambda i: ops.attention_split(q, *caches[i % nrot], slot, kvlen, out=out, waves=nw, splits=ns,
+                                                      workspace=wsp))
             for k, (med, mn) in res.items():
                 print(json.dumps({"M": M, "op": f"attn_T{T}", "variant": k, "us": round(med, 2), "us_min": round(mn, 2),
                                   "GBps": round(kv_bytes / med / 1e3, 1)}), flush=True)

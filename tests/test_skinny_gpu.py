@@ -168,6 +168,37 @@ def test_attention_split(B, T, waves):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("B,T", [(1, 1024), (8, 1024), (2, 700), (3, 150)])
+@pytest.mark.parametrize("waves,splits", [(4, 3), (4, 8), (2, 16), (8, 64), (4, 0)])
+@pytest.mark.parametrize("sync", [0, 2])
+def test_attention_split_across_workgroups(B, T, waves, splits, sync):
+    """Keys split over several workgroups per (row, head), merged by the last to arrive: matches
+    fp32 at T=1024 / B=1 and 8 (splits=0: the engine's geometry); re-running on the same
+    workspace (counters re-armed by the kernel) gives bit-identical output."""
+    ops = _ops()
+    H, S = 12, max(B, 4)
+    if splits == 0:
+        waves, splits = ops.attention_split_geometry(B * H, T)
+    kc = _rand(S, H, T, 64, seed=91)
+    vc = _rand(S, H, T, 64, seed=92)
+    q = _rand(B, H * 64, seed=93)
+    gen = torch.Generator().manual_seed(94)
+    slot = torch.randperm(S, generator=gen)[:B].to(torch.int32).to(DEV)
+    kvlen = torch.randint(1, T + 1, (B,), generator=gen)
+    kvlen[0] = T
+    if B > 2:
+        kvlen[1] = 1  # most workgroups of this row see no keys
+    kvlen = kvlen.to(torch.int32).to(DEV)
+    ws = ops.AttnSplitWorkspace(B * H, splits, DEV)
+    out = ops.attention_split(q, kc, vc, slot, kvlen, waves=waves, splits=splits, workspace=ws, sync=sync)
+    ref = _attn_ref(q, kc, vc, slot, kvlen)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    assert int(ws.counters.abs().sum()) == 0
+    for _ in range(3):
+        again = ops.attention_split(q, kc, vc, slot, kvlen, waves=waves, splits=splits, workspace=ws, sync=sync)
+        assert torch.equal(again, out)
+
+
 def test_attention_split_matches_wave_kernel():
     """Split-K and the one-wave-per-(row, head) kernel agree (same online-softmax numerics)."""
     ops = _ops()
