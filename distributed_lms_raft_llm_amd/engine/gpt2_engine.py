@@ -133,6 +133,9 @@ class HipGPT2Engine:
     # (row, head) pairs up to which decode attention uses the split-K kernel (profiles/r2_skinny_bench.log:
     # at 32 rows x 12 heads, T=150: 7.9 us vs 12.3 us for one wave per pair)
     SPLIT_ATTN_MAX_PAIRS = 1024
+    # fused attention + out-projection up to this many rows: batch 1 40.6 vs 43.3 ms per query,
+    # batch 4 48.0 vs 47.3 (its workgroups recompute a head's attention per row)
+    FUSE_AO_MAX_ROWS = 2
     # split-K of the row-parallel projections on the latency path (fixed: the fused add+LN
     # kernel sums exactly this many slabs)
     SMALL_SPLIT = 4
@@ -223,6 +226,23 @@ class HipGPT2Engine:
                 if lw.w_qkv_sh is None:
                     lw.w_qkv_sh = ops.shuffle_weight(lw.w_qkv)
                     lw.w_fc_sh = ops.shuffle_weight(lw.w_fc)
+        # attention fused with the out-projection for <= 4 rows (one launch fewer per layer); its
+        # workgroups recompute a head's attention, so only for short caches
+        # (TP=1: its per-head slabs are summed by the next fused add+LN kernel, 12 or 16 of them)
+        self.fuse_ao = (self.small_max > 0 and self.tp_size == 1 and self.max_length <= 512 and
+                        self.w.n_heads_local in (12, 16) and cfg.n_embd <= 1024 and
+                        os.environ.get("DLMS_FUSE_ATTN_OPROJ", "1") != "0")
+        if self.fuse_ao:
+            try:
+                ops.attention_oproj_tiles(cfg.n_embd)
+            except ValueError:
+                self.fuse_ao = False
+        self.ao_parts = None
+        if self.fuse_ao:
+            for lw in self.w.layers:
+                if lw.w_o_sh is None:
+                    lw.w_o_sh = ops.shuffle_weight(lw.w_o)
+            self.ao_parts = torch.zeros(self.w.n_heads_local, 4, cfg.n_embd, dtype=torch.float32, device=self.device)
         # LM head of the throughput path (>= PS_LM_MIN_ROWS rows): panel-resident gemm_ps on a
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
@@ -583,10 +603,14 @@ class HipGPT2Engine:
                                       parts=parts, nsplit=pend[0], res_bias=pend[1], bias=lw.b_qkv, q_out=r.q,
                                       k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
                 cur = 1 - cur
-            self._attn(r, li)
-            ns = row_parallel(r.att, lw.w_o)
+            if self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
+                ops.attention_oproj(self.q[:B], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts)
+                mlp_parts, ns = self.ao_parts[:, :B], self.w.n_heads_local
+            else:
+                self._attn(r, li)
+                mlp_parts, ns = parts, row_parallel(r.att, lw.w_o)
             ops.skinny_addln_gemm(bufs[cur], lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps,
-                                  x_out=bufs[1 - cur], parts=parts, nsplit=ns, res_bias=lw.b_o, bias=lw.b_fc,
+                                  x_out=bufs[1 - cur], parts=mlp_parts, nsplit=ns, res_bias=lw.b_o, bias=lw.b_fc,
                                   out=r.ff)
             cur = 1 - cur
             pend = (row_parallel(r.ff, lw.w_p), lw.b_p)

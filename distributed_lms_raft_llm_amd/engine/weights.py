@@ -58,6 +58,7 @@ class LayerWeights:
     # skinny kernels; filled by the engine when that path is enabled
     w_qkv_sh: torch.Tensor | None = None
     w_fc_sh: torch.Tensor | None = None
+    w_o_sh: torch.Tensor | None = None  # fused attention + out-projection (B <= 4)
 
 
 @dataclass

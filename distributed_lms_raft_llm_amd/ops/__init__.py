@@ -130,6 +130,7 @@ def _bind(L):
         "dlms_cosine": [P, P, P, I, I, I, F, P],
         "dlms_skinny_gemm": [I, P, I, P, P, F, P, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_attention_split": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, I, P, P, I, P],
+        "dlms_attention_oproj": [P, I, P, P, P, P, I, I, I, I, F, P, I, I, P, I, ctypes.c_longlong, P],
         "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
                                    ctypes.POINTER(GemmEpi), P],
         "dlms_skinny_addln_max_rows": [I],
@@ -789,7 +790,8 @@ def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, b
         out = epi(bf16(LN(v)) @ W.T + bias)
 
     ``x_out`` must not alias ``x_in`` (every workgroup re-reads x_in; one of them writes x_out):
-    the engine ping-pongs two residual buffers.  nsplit in {0, 1, 4}."""
+    the engine ping-pongs two residual buffers.  nsplit in {0, 1, 4}, or 12 / 16 (per-head slabs of
+    ``attention_oproj``; M <= 4, K <= 1024)."""
     _req(x_in, torch.float32, "x_in", 2)
     _req(w_sh, torch.bfloat16, "w_sh", 4)
     G, KB = w_sh.shape[0], w_sh.shape[1]
@@ -803,8 +805,10 @@ def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, b
         _req(t, torch.float32, n, 1)
         if t.numel() != K:
             raise ValueError(f"{n} size")
-    if nsplit not in (0, 1, 4):
-        raise ValueError("skinny_addln_gemm: nsplit in {0, 1, 4}")
+    if nsplit not in (0, 1, 4, 12, 16):
+        raise ValueError("skinny_addln_gemm: nsplit in {0, 1, 4, 12, 16}")
+    if nsplit > 4 and (x_in.shape[0] > 4 or x_in.shape[1] > 1024):
+        raise ValueError("skinny_addln_gemm: 12/16 slabs only for <= 4 rows of width <= 1024")
     ldp, sstride = 0, 0
     if nsplit:
         _req(parts, torch.float32, "parts", 3)
@@ -938,6 +942,50 @@ def attention_split(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                                       ws_p, cnt_p, ATTN_SPLIT_SYNC if sync is None else int(sync), _stream()),
            "attention_split")
     return out
+
+
+def attention_oproj_tiles(n_out: int, target_wgs: int = 16) -> int:
+    """16-column output tiles per workgroup for ``attention_oproj``: the divisor of N/16 in
+    {2,3,4,5,6,8} whose workgroups-per-head count is closest to ``target_wgs``."""
+    G = n_out // 16
+    cands = [nt for nt in (2, 3, 4, 5, 6, 8) if G % nt == 0]
+    if not cands:
+        raise ValueError(f"attention_oproj: N/16 = {G} has no tile count in (2,3,4,5,6,8)")
+    return min(cands, key=lambda nt: (abs(G // nt - target_wgs), nt))
+
+
+def attention_oproj(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
+                    row_kvlen: torch.Tensor, wo_sh: torch.Tensor, parts: torch.Tensor, scale: float | None = None,
+                    tiles: int | None = None) -> torch.Tensor:
+    """Decode attention fused with the out-projection (M <= 4 rows): head h's share
+    ``attn_h(q) @ W_o[:, 64h:64h+64]^T`` goes to ``parts[h, :M, :N]`` (fp32 split-K slabs; no bias),
+    so ``parts[:H].sum(0)`` is the out-projection -- what the next fused add+LN kernel sums with
+    ``nsplit=H``.  ``wo_sh`` is ``shuffle_weight(W_o)`` with W_o [N, H*64]."""
+    _req(q, torch.bfloat16, "q", 2)
+    _req(k_cache, torch.bfloat16, "k_cache", 4)
+    _req(v_cache, torch.bfloat16, "v_cache", 4)
+    _req(row_slot, torch.int32, "row_slot", 1)
+    _req(row_kvlen, torch.int32, "row_kvlen", 1)
+    _req(wo_sh, torch.bfloat16, "wo_sh", 4)
+    _req(parts, torch.float32, "parts", 3)
+    M = q.shape[0]
+    S, H, T, hd = k_cache.shape
+    N = wo_sh.shape[0] * 16
+    if not 1 <= M <= 4:
+        raise ValueError("attention_oproj: 1..4 rows")
+    if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64 or wo_sh.shape[1] * 32 != H * 64:
+        raise ValueError("attention_oproj: bad shapes")
+    if parts.shape[0] < H or parts.shape[1] < M or parts.shape[2] < N or parts.stride(2) != 1:
+        raise ValueError("attention_oproj: parts must be [>= H, >= M, >= N]")
+    if row_slot.numel() < M or row_kvlen.numel() < M:
+        raise ValueError("attention_oproj: index arrays too short")
+    nt = attention_oproj_tiles(N) if tiles is None else tiles
+    sc = (1.0 / 8.0) if scale is None else scale
+    _check(lib().dlms_attention_oproj(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen), M,
+                                      H, T, S, float(sc), _p(wo_sh), N, int(nt), _p(parts), parts.stride(1),
+                                      parts.stride(0), _stream()),
+           "attention_oproj")
+    return parts
 
 
 # ---------------------------------------------------------------------------------------------

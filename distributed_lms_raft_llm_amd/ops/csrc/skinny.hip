@@ -509,7 +509,7 @@ static hipError_t addln_rpw(const float* x_in, float* x_out, int ldx, const floa
                             const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M, int N,
                             int K, const GemmEpi& ep, hipStream_t stream) {
     if (M <= 4) return launch_addln<EPI, NSPLIT, NV4, 1>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-    if constexpr (NV4 <= 4) {
+    if constexpr (NV4 <= 4 && NSPLIT <= 4) {
         if (M <= 8) return launch_addln<EPI, NSPLIT, NV4, 2>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
     }
     return hipErrorInvalidValue;
@@ -519,6 +519,13 @@ template <int EPI, int NSPLIT>
 static hipError_t addln_nv4(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
                             const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M, int N,
                             int K, const GemmEpi& ep, hipStream_t stream) {
+    if constexpr (NSPLIT > 4) {  // per-head slabs of the fused attention + out-projection (M <= 4, K <= 1024)
+        switch ((K / 4 + 63) / 64) {
+            case 3: return addln_rpw<EPI, NSPLIT, 3>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+            case 4: return addln_rpw<EPI, NSPLIT, 4>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch ((K / 4 + 63) / 64) {
         case 1: return addln_rpw<EPI, NSPLIT, 1>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
         case 2: return addln_rpw<EPI, NSPLIT, 2>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
@@ -550,6 +557,8 @@ extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const float* x_in, float* 
         case 0: ADDLN(E, 0);            \
         case 1: ADDLN(E, 1);            \
         case 4: ADDLN(E, 4);            \
+        case 12: ADDLN(E, 12);          \
+        case 16: ADDLN(E, 16);          \
         default: return hipErrorInvalidValue; \
     }
     switch (epi) {
@@ -708,8 +717,8 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
     // last-arriver merge (stream-K fix-up): publish our partial device-wide, count arrivals;
     // the workgroup that arrives last merges all NS partials and re-arms the counter.  Nobody
     // waits on anybody, so there is no co-residency assumption.
-    if (SYNC == 2)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // our coherent stores are complete
+    if (SYNC == 2)  // our write-through stores have all been acknowledged (explicit: the compiler
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // emits no wait for a workgroup fence)
     else
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     int old = 0;
@@ -762,6 +771,189 @@ extern "C" hipError_t dlms_attention_split(const void* q, int ldq, const void* k
             : sync == 1 ? pick(std::integral_constant<int, 1>{})
                         : pick(std::integral_constant<int, 2>{});
     if (!ok) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Attention + out-projection in ONE kernel (latency path, M <= 4 rows).
+//
+// The batch-1 layer is a chain of latency-bound launches; this removes one: workgroup (h, j)
+// computes head h's attention for all M rows (its keys split over the 4 waves, log-sum-exp merge in
+// LDS) and multiplies the 64-wide result by its NT 16-column tiles of W_o (pre-shuffled; the tiles'
+// k-blocks 2h, 2h+1 are loaded at kernel start, under the attention).  The J = N / (16 NT)
+// workgroups of a head recompute the same attention (a few KB of K/V per row at GPT-2 lengths,
+// L2-served) so that the out-projection's weights are spread over H * J workgroups.  Head h's
+// contribution goes to split-K slab h with plain stores; the next fused add+LN kernel sums the H
+// slabs in fixed order (deterministic).  (Summing them here instead -- write-through partials +
+// an arrival counter + last-arriver reduce -- measured 11.8 us per call against 5.5 + 5.1 for the
+// two kernels it replaced: three dependent global round trips cost what a launch boundary does.)
+template <int NT>
+__global__ __launch_bounds__(256) void attn_oproj_kernel(
+    const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ row_slot, const int* __restrict__ row_kvlen, int M, int H, int t_max, int n_slots,
+    float scale_log2, const bf16_t* __restrict__ Wo_sh, int N, float* __restrict__ part, int ldp,
+    long long split_stride) {
+    constexpr int NW = 4;
+    constexpr int TPW = (NT + NW - 1) / NW;  // output tiles per wave
+    constexpr int U = 8;                      // key groups of 8 in flight per wave
+    __shared__ float part_s[NW][8][10];
+    __shared__ __attribute__((aligned(16))) bf16_t aimg[16][72];  // o as the MFMA A operand, padded rows
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = blockIdx.x;
+    const int j = blockIdx.y;
+    const int nkb = (H * 64) >> 5;
+
+    // (0) this workgroup's W_o fragments first: they do not depend on the attention
+    bf16x8_t wb[TPW][2];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = wave + NW * i < NT ? wave + NW * i : NT - 1;
+        const bf16x8_t* src = reinterpret_cast<const bf16x8_t*>(Wo_sh) + ((size_t)(j * NT + t) * nkb + 2 * h) * 64 + lane;
+        wb[i][0] = src[0];
+        wb[i][1] = src[64];
+    }
+
+    // (1) attention of head h: S = 4 / M waves per row
+    const int S = M == 1 ? 4 : (M == 2 ? 2 : 1);
+    const int row = wave / S;
+    const int sl = wave - row * S;
+    const int g = lane >> 3;
+    const int c = lane & 7;
+    float m = -INFINITY, l = 0.f;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (row < M) {
+        const int slot = (int)dlms_idx(row_slot[row], n_slots, CHK_ATTN_SLOT);
+        int kvlen = row_kvlen[row];
+        kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
+        const int span = ((kvlen + S - 1) / S + 7) & ~7;
+        const int t_lo = sl * span < kvlen ? sl * span : kvlen;
+        const int t_hi = t_lo + span < kvlen ? t_lo + span : kvlen;
+        const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+        const bf16_t* K = kc + head_off + c * 8;
+        const bf16_t* V = vc + head_off + c * 8;
+        float qf[8];
+        unpack8(*reinterpret_cast<const uint4*>(q + (size_t)row * ldq + h * 64 + c * 8), qf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[e] *= scale_log2;
+        for (int t0 = t_lo; t0 < t_hi; t0 += 8 * U) {
+            uint4 kr[U], vr[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int t = t0 + u * 8 + g;
+                t = t < t_hi ? t : t_hi - 1;
+                kr[u] = *reinterpret_cast<const uint4*>(K + (size_t)t * 64);
+                vr[u] = *reinterpret_cast<const uint4*>(V + (size_t)t * 64);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float kf[8];
+                unpack8(kr[u], kf);
+                float sc = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sc += qf[e] * kf[e];
+                sc += __shfl_xor(sc, 1, 64);
+                sc += __shfl_xor(sc, 2, 64);
+                sc += __shfl_xor(sc, 4, 64);
+                if (t0 + u * 8 + g < t_hi) {
+                    const float m_new = fmaxf(m, sc);
+                    const float corr = exp2f(m - m_new);
+                    const float p = exp2f(sc - m_new);
+                    float vf[8];
+                    unpack8(vr[u], vf);
+                    l = l * corr + p;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) acc[e] = acc[e] * corr + p * vf[e];
+                    m = m_new;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+        const float m_o = __shfl_xor(m, o, 64);
+        const float l_o = __shfl_xor(l, o, 64);
+        const float m_n = fmaxf(m, m_o);
+        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
+        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
+        l = l * a + l_o * b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + __shfl_xor(acc[e], o, 64) * b;
+        m = m_n;
+    }
+    if (g == 0) {
+        part_s[wave][c][0] = m;
+        part_s[wave][c][1] = l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part_s[wave][c][2 + e] = acc[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) {  // (row r, 8-dim chunk cc) -> bf16 A image; rows >= M are zero
+        const int r = threadIdx.x >> 3, cc = threadIdx.x & 7;
+        float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (r < M) {
+            float M_ = -INFINITY;
+            for (int w = r * S; w < r * S + S; ++w) M_ = fmaxf(M_, part_s[w][cc][0]);
+            float L = 0.f;
+            for (int w = r * S; w < r * S + S; ++w) {
+                const float mw = part_s[w][cc][0];
+                if (mw == -INFINITY) continue;
+                const float f = exp2f(mw - M_);
+                L += part_s[w][cc][1] * f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o8[e] += part_s[w][cc][2 + e] * f;
+            }
+            const float inv = 1.f / L;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o8[e] *= inv;
+        }
+        *reinterpret_cast<uint4*>(&aimg[r][cc * 8]) = pack8(o8);
+    }
+    __syncthreads();
+
+    // (2) o[16 x 64] . W_o[tile cols, head h's 64 k]^T on MFMA -> slab h
+    const int fr = lane & 15, gg = lane >> 4;
+    const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(&aimg[fr][gg * 8]);
+    const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(&aimg[fr][32 + gg * 8]);
+    float* slab = part + (size_t)h * split_stride;
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = wave + NW * i;
+        if (t >= NT) continue;  // wave-uniform
+        f32x4_t d = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wb[i][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wb[i][1], d, 0, 0, 0);
+        const int col = (j * NT + t) * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rr = gg * 4 + r;
+            if (rr < M) slab[(size_t)rr * ldp + col] = d[r];
+        }
+    }
+}
+
+extern "C" hipError_t dlms_attention_oproj(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
+                                           const int* row_kvlen, int M, int H, int t_max, int n_slots, float scale,
+                                           const void* wo_sh, int N, int nt, float* part, int ldp,
+                                           long long split_stride, hipStream_t stream) {
+    if (M < 1 || M > 4 || H < 1 || t_max < 1 || N % 16 || nt < 1 || (N / 16) % nt) return hipErrorInvalidValue;
+    const float sl2 = scale * 1.4426950408889634f;
+    const dim3 grid(H, (N / 16) / nt);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
+                           reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
+                           row_kvlen, M, H, t_max, n_slots, sl2, reinterpret_cast<const bf16_t*>(wo_sh), N, part,
+                           ldp, split_stride);
+    };
+    switch (nt) {
+        case 2: go(attn_oproj_kernel<2>); break;
+        case 3: go(attn_oproj_kernel<3>); break;
+        case 4: go(attn_oproj_kernel<4>); break;
+        case 5: go(attn_oproj_kernel<5>); break;
+        case 6: go(attn_oproj_kernel<6>); break;
+        case 8: go(attn_oproj_kernel<8>); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

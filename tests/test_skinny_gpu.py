@@ -199,6 +199,52 @@ def test_attention_split_across_workgroups(B, T, waves, splits, sync):
         assert torch.equal(again, out)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("H,T", [(12, 150), (12, 37), (16, 512), (20, 150), (25, 100)])
+def test_attention_oproj(M, H, T):
+    """Fused decode attention + out-projection: slab h == fp32 attention of head h -> bf16 ->
+    @ W_o[:, head h]^T, and the slabs sum to the full out-projection."""
+    ops = _ops()
+    N, S = H * 64, 6
+    kc, vc = _rand(S, H, T, 64, seed=101), _rand(S, H, T, 64, seed=102)
+    q = _rand(M, H * 64, seed=103)
+    wo = _rand(N, H * 64, scale=0.05, seed=104)
+    gen = torch.Generator().manual_seed(105)
+    slot = torch.randperm(S, generator=gen)[:M].to(torch.int32).to(DEV)
+    kvlen = torch.randint(1, T + 1, (M,), generator=gen)
+    kvlen[0] = T
+    kvlen = kvlen.to(torch.int32).to(DEV)
+    parts = torch.full((H, 4, N), 7.0, device=DEV)
+    ops.attention_oproj(q, kc, vc, slot, kvlen, ops.shuffle_weight(wo), parts)
+    o = _attn_ref(q, kc, vc, slot, kvlen).to(torch.bfloat16).float().reshape(M, H, 64)
+    for h in range(H):
+        ref_h = o[:, h] @ wo.float()[:, 64 * h:64 * h + 64].t()
+        torch.testing.assert_close(parts[h, :M], ref_h, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(parts[:, :M].sum(0), o.reshape(M, -1) @ wo.float().t(), atol=5e-2, rtol=2e-2)
+    assert torch.all(parts[:, M:] == 7.0)  # rows >= M untouched
+
+
+@pytest.mark.parametrize("ns", [12, 16])
+def test_skinny_addln_many_slabs(ns):
+    """The fused add+LN consumes 12 / 16 per-head slabs (fixed order) like 4."""
+    ops = _ops()
+    M, K, N = 3, 768 if ns == 12 else 1024, 3072
+    x = _rand(M, K, seed=111, dtype=torch.float32)
+    parts = _rand(ns, M, K, seed=112, dtype=torch.float32) * 0.3
+    rb = _rand(K, seed=113, dtype=torch.float32)
+    g, b = _rand(K, seed=114, dtype=torch.float32), _rand(K, seed=115, dtype=torch.float32)
+    w = _rand(N, K, scale=0.05, seed=116)
+    bias = _rand(N, seed=117, dtype=torch.float32) * 0.1
+    x_out = torch.zeros_like(x)
+    out = ops.skinny_addln_gemm(x, ops.shuffle_weight(w), ops.EPI_GELU_TANH, g, b, 1e-5, x_out=x_out, parts=parts,
+                                nsplit=ns, res_bias=rb, bias=bias)
+    v = x + rb + parts.sum(0)
+    torch.testing.assert_close(x_out, v, atol=1e-5, rtol=1e-5)
+    h = _ln_ref(v, g, b, 1e-5).to(torch.bfloat16).float()
+    ref = torch.nn.functional.gelu(h @ w.float().t() + bias, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 def test_attention_split_matches_wave_kernel():
     """Split-K and the one-wave-per-(row, head) kernel agree (same online-softmax numerics)."""
     ops = _ops()
