@@ -1,0 +1,65 @@
+#!/bin/bash
+# One entry point for the GPU-box work of this repo (replaces the per-experiment lease scripts):
+#
+#   gpurun -- bash scripts/gpu_tasks.sh <task> [<task> ...]
+#
+# tasks (run in order; the first failing step ends the call -- no GPU work after a fault/timeout):
+#   tests            full `pytest -m gpu` tier                     -> gpurun_out/tests.log
+#   smoke            __graft_entry__.smoke()
+#   bench            default bench.py (headline + b1/b32 keys)    -> gpurun_out/bench.log
+#   prof:<tag>       rocprofv3 kernel stats of a short bench.py run (B=1024)   -> gpurun_out/prof_<tag>/
+#   prof1:<tag>      the same at batch 1
+#   skinny           latency-path kernel microbench                -> gpurun_out/skinny.jsonl
+#   attn             split-K flash-decode sweep (B x T x waves x workgroups)   -> gpurun_out/attn.jsonl
+#   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
+#   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
+#   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+T="python -u -m pytest -x -q --timeout 180 --timeout-method thread"
+
+step() {  # step <seconds> <log> <cmd...>: own time limit; a fault, abort or timeout ends the call
+    local secs=$1 log=$2
+    shift 2
+    echo "=== $(date +%T) $*" >> "$log"
+    timeout -k 10 "$secs" "$@" >> "$log" 2>&1
+    local rc=$?
+    echo "=== rc=$rc" >> "$log"
+    [ $rc -ne 0 ] && { echo "step failed rc=$rc: $*" >&2; tail -5 "$log" >&2; exit $rc; }
+    return 0
+}
+
+prof() {  # prof <tag> <bench args...>
+    local tag=$1
+    shift
+    export TMPDIR=/tmp
+    mkdir -p gpurun_out/prof_$tag
+    step 300 gpurun_out/prof_$tag/bench.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run \
+        --output-format csv -- python3 bench.py "$@"
+    find gpurun_out/prof_$tag -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/prof_$tag/kernel_stats.csv
+    find gpurun_out/prof_$tag -name "*_kernel_trace.csv" -delete
+    python scripts/kstats.py gpurun_out/prof_$tag/kernel_stats.csv > gpurun_out/prof_$tag/summary.txt
+    head -12 gpurun_out/prof_$tag/summary.txt
+}
+
+for task in "$@"; do
+    case "$task" in
+        tests) step 900 gpurun_out/tests.log $T -m gpu tests/; tail -2 gpurun_out/tests.log ;;
+        smoke) step 300 gpurun_out/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; tail -2 gpurun_out/smoke.log ;;
+        bench) step 600 gpurun_out/bench.log python -u bench.py; grep '^{' gpurun_out/bench.log | tail -1 ;;
+        prof:*) prof "${task#prof:}" --steps 5 --warmup 2 --latency-batches "" ;;
+        prof1:*) prof "${task#prof1:}" --batch 1 --steps 3 --warmup 1 --latency-batches "" ;;
+        skinny) step 300 gpurun_out/skinny.jsonl python -u scripts/bench_skinny.py ;;
+        attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
+        ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
+        gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;
+        sweep:*)
+            IFS=';' read -ra sets <<< "${task#sweep:}"
+            for envs in "${sets[@]}"; do
+                step 300 gpurun_out/sweep.log env ${envs//,/ } python -u bench.py --steps 5 --warmup 2 --latency-batches ""
+                echo "{\"env\": \"$envs\", \"bench\": $(grep '^{' gpurun_out/sweep.log | tail -1)}" >> gpurun_out/sweep.jsonl
+                tail -1 gpurun_out/sweep.jsonl
+            done ;;
+        *) echo "unknown task $task" >&2; exit 2 ;;
+    esac
+done
