@@ -13,6 +13,8 @@
 #   attn             split-K flash-decode sweep (B x T x waves x workgroups)   -> gpurun_out/attn.jsonl
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
+#   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
+#   e2e:<n>          scripts/run_config.py --config n (Raft cluster + gate + tutor) -> gpurun_out/e2e_<n>.log
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -53,6 +55,10 @@ for task in "$@"; do
         attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
         gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;
+        serving) step 400 gpurun_out/serving.jsonl python -u scripts/bench_serving.py --rates 20,200,1000 --queries 400 \
+                     --modes continuous; grep '^{' gpurun_out/serving.jsonl ;;
+        e2e:*) step 900 gpurun_out/e2e_${task#e2e:}.log python -u scripts/run_config.py --config ${task#e2e:}
+               tail -3 gpurun_out/e2e_${task#e2e:}.log ;;
         sweep:*)
             IFS=';' read -ra sets <<< "${task#sweep:}"
             for envs in "${sets[@]}"; do
