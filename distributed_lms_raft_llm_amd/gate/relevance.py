@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import hashlib
 import logging
+import os
 import threading
 import time
 from collections import OrderedDict
@@ -60,6 +61,10 @@ class RelevanceGate:
             from ..engine.bert_engine import HipBertEncoder
 
             enc = HipBertEncoder(cfg, w, device=device)
+            if os.environ.get("DLMS_GATE_WARM", "1") != "0":
+                t0 = time.perf_counter()
+                n = enc.warm_graphs()
+                log.info("relevance gate: %d encoder graphs captured in %.2f s", n, time.perf_counter() - t0)
         else:
             enc = BertReference(cfg, w, device="cpu")
         tok = BertWordPiece(vocab, vocab_size=cfg.vocab_size, max_length=cfg.max_position)

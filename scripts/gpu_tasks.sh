@@ -5,6 +5,7 @@
 #
 # tasks (run in order; the first failing step ends the call -- no GPU work after a fault/timeout):
 #   tests            full `pytest -m gpu` tier                     -> gpurun_out/tests.log
+#   test:<path>      one test file / node id of the gpu tier       -> gpurun_out/test_sel.log
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench.py (headline + b1/b32 keys)    -> gpurun_out/bench.log
 #   prof:<tag>       rocprofv3 kernel stats of a short bench.py run (B=1024)   -> gpurun_out/prof_<tag>/
@@ -47,6 +48,7 @@ prof() {  # prof <tag> <bench args...>
 for task in "$@"; do
     case "$task" in
         tests) step 900 gpurun_out/tests.log $T -m gpu tests/; tail -2 gpurun_out/tests.log ;;
+        test:*) step 600 gpurun_out/test_sel.log $T -m gpu ${task#test:}; tail -2 gpurun_out/test_sel.log ;;
         smoke) step 300 gpurun_out/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; tail -2 gpurun_out/smoke.log ;;
         bench) step 600 gpurun_out/bench.log python -u bench.py; grep '^{' gpurun_out/bench.log | tail -1 ;;
         prof:*) prof "${task#prof:}" --steps 5 --warmup 2 --latency-batches "" ;;

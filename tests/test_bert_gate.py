@@ -131,3 +131,26 @@ def test_hip_gate_batched_at_512_tokens():
         r = torch.nn.functional.cosine_similarity(qe, a).item()
         assert abs(s - r) < 2e-3, (q[:20], s, r)
     assert gate.passes < len(queries)
+
+
+@pytest.mark.gpu
+def test_hip_encoder_graph_buckets_match_eager():
+    """hipGraph-replayed passes (rows padded to a power-of-two bucket by dummy sequences, tile table
+    padded by repeating its last tile) == the eager packed pass, across buckets and re-used buckets
+    with different length mixes."""
+    from distributed_lms_raft_llm_amd.engine.bert_engine import HipBertEncoder
+
+    cfg, w = _weights("bert-base-uncased")
+    graphed = HipBertEncoder(cfg, w, use_graph=True)
+    eager = HipBertEncoder(cfg, w, use_graph=False)
+    g = torch.Generator().manual_seed(7)
+    mixes = [(5,), (40, 3, 17), (64,), (33, 31), (1, 1, 1, 1, 1), (512, 7), (300, 250, 100), (12,) * 40]
+    for lens in mixes + mixes[:3]:
+        batch = [torch.randint(110, cfg.vocab_size, (L,), generator=g).tolist() for L in lens]
+        a = graphed.embed(batch).cpu()
+        b = eager.embed(batch).cpu()
+        assert a.shape == b.shape == (len(lens), cfg.hidden)
+        cos = torch.nn.functional.cosine_similarity(a, b, dim=1)
+        assert cos.min().item() > 0.9999, (lens, cos)
+        torch.testing.assert_close(a, b, atol=2e-2, rtol=2e-2)
+    assert len(graphed._gstate) >= 3 and all(st["graph"] is not None for st in graphed._gstate.values())
