@@ -214,6 +214,7 @@ class HipGPT2Engine:
         # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
         self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "0"))
         self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
+        self.alt_attn = os.environ.get("DLMS_OVERLAP_ALT_ATTN", "0") == "1"
         if self.overlap_parts not in (2, 3, 4):
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
         if latency_path is None:
@@ -535,12 +536,38 @@ class HipGPT2Engine:
         parts = [(i * step, self._part_rows(i * step, (i + 1) * step)) for i in range(k)]
         if k == 2 and os.environ.get("DLMS_OVERLAP_SERIAL", "0") == "1":
             self._two_halves_serialised(parts, streams, penalty)
+        elif self.alt_attn:
+            self._alternating_attention(parts, streams, penalty)
         else:
             for (lo, r), s in zip(parts, streams):
                 with torch.cuda.stream(s):
                     self._part_step(r, lo, penalty)
         for s in streams[1:]:
             cur.wait_stream(s)
+
+    def _alternating_attention(self, parts, streams, penalty: float):
+        """Attention kernels of the row ranges take turns on HBM (part 0 layer l, part 1 layer l, ...,
+        part 0 layer l + 1): each waits for the previous one to finish, so the KV stream of one part
+        always runs beside the GEMM-side chain of the others instead of all parts' attentions
+        colliding at the same time (free-running identical chains fall into phase)."""
+        last = None
+        for li in range(len(self.w.layers)):
+            for (lo, r), s in zip(parts, streams):
+                with torch.cuda.stream(s):
+                    self._attn_in(r, li)
+                    if last is not None:
+                        s.wait_event(last)
+                    self._attn(r, li)
+                    last = torch.cuda.Event()
+                    last.record(s)
+                    self._attn_out_mlp(r, li)
+        for (lo, r), s in zip(parts, streams):
+            with torch.cuda.stream(s):
+                self._final_ln(r, r.h)
+                if self.w.fp8:
+                    self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
+                else:
+                    self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
 
     def _two_halves_serialised(self, halves, streams, penalty: float):
         """Phases G(0) A(0) G(1) ... A(L-1) G(L) per half (G(l) = out-proj/LN2/c_fc/c_proj of

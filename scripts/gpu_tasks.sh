@@ -10,6 +10,7 @@
 #   bench            default bench.py (headline + b1/b32 keys)    -> gpurun_out/bench.log
 #   prof:<tag>       rocprofv3 kernel stats of a short bench.py run (B=1024)   -> gpurun_out/prof_<tag>/
 #   prof1:<tag>      the same at batch 1
+#   trace:<tag>      per-dispatch kernel trace of one B=1024 generation (timeline analysis) -> gpurun_out/trace_<tag>/
 #   skinny           latency-path kernel microbench                -> gpurun_out/skinny.jsonl
 #   attn             split-K flash-decode sweep (B x T x waves x workgroups)   -> gpurun_out/attn.jsonl
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
@@ -53,6 +54,13 @@ for task in "$@"; do
         bench) step 600 gpurun_out/bench.log python -u bench.py; grep '^{' gpurun_out/bench.log | tail -1 ;;
         prof:*) prof "${task#prof:}" --steps 5 --warmup 2 --latency-batches "" ;;
         prof1:*) prof "${task#prof1:}" --batch 1 --steps 3 --warmup 1 --latency-batches "" ;;
+        trace:*)
+            tag=${task#trace:}; export TMPDIR=/tmp; mkdir -p gpurun_out/trace_$tag
+            step 300 gpurun_out/trace_$tag/bench.log rocprofv3 --kernel-trace -d gpurun_out/trace_$tag -o run \
+                --output-format csv -- python3 bench.py --steps 1 --warmup 1 --latency-batches ""
+            f=$(find gpurun_out/trace_$tag -name "*kernel_trace.csv" | head -1)
+            step 120 gpurun_out/trace_$tag/timeline.txt python scripts/timeline.py "$f"
+            gzip -f "$f"; cat gpurun_out/trace_$tag/timeline.txt ;;
         skinny) step 300 gpurun_out/skinny.jsonl python -u scripts/bench_skinny.py ;;
         attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
