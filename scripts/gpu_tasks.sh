@@ -10,6 +10,8 @@
 #   bench            default bench.py (headline + b1/b32 keys)    -> gpurun_out/bench.log
 #   prof:<tag>       rocprofv3 kernel stats of a short bench.py run (B=1024)   -> gpurun_out/prof_<tag>/
 #   prof1:<tag>      the same at batch 1
+#   pmc:<tag>:<batch>  three rocprofv3 --pmc passes (SQ / TCC fetch / TCC write) of an eager bench.py run
+#                    -> gpurun_out/pmc_<tag>/summary.json
 #   trace:<tag>      per-dispatch kernel trace of one B=1024 generation (timeline analysis) -> gpurun_out/trace_<tag>/
 #   skinny           latency-path kernel microbench                -> gpurun_out/skinny.jsonl
 #   attn             split-K flash-decode sweep (B x T x waves x workgroups)   -> gpurun_out/attn.jsonl
@@ -54,6 +56,19 @@ for task in "$@"; do
         bench) step 600 gpurun_out/bench.log python -u bench.py; grep '^{' gpurun_out/bench.log | tail -1 ;;
         prof:*) prof "${task#prof:}" --steps 5 --warmup 2 --latency-batches "" ;;
         prof1:*) prof "${task#prof1:}" --batch 1 --steps 3 --warmup 1 --latency-batches "" ;;
+        pmc:*)
+            spec=${task#pmc:}; tag=${spec%%:*}; batch=${spec#*:}; export TMPDIR=/tmp; D=gpurun_out/pmc_$tag; mkdir -p $D
+            passes=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
+                    "FETCH_SIZE TCC_HIT_sum" "WRITE_SIZE TCC_MISS_sum")
+            i=0
+            for ctrs in "${passes[@]}"; do
+                i=$((i + 1))
+                step 240 $D/pass$i.log timeout -s KILL 200 rocprofv3 --pmc $ctrs -d $D/p$i -o run --output-format csv \
+                    -- python3 bench.py --batch $batch --steps 1 --warmup 0 --no-graph --latency-batches ""
+            done
+            step 120 $D/summary.txt python scripts/pmc_summary.py $D/summary.json $(find $D -name "*counter_collection.csv")
+            find $D -name "*counter_collection.csv" -delete
+            cat $D/summary.txt ;;
         trace:*)
             tag=${task#trace:}; export TMPDIR=/tmp; mkdir -p gpurun_out/trace_$tag
             step 300 gpurun_out/trace_$tag/bench.log rocprofv3 --kernel-trace -d gpurun_out/trace_$tag -o run \
