@@ -215,6 +215,9 @@ class HipGPT2Engine:
         self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "0"))
         self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
         self.alt_attn = os.environ.get("DLMS_OVERLAP_ALT_ATTN", "0") == "1"
+        self.prefill_graphs = os.environ.get("DLMS_PREFILL_GRAPH", "1") != "0"
+        self._pgraphs: dict[tuple[int, int], dict] = {}
+        self._pseen: dict[tuple[int, int], int] = {}
         if self.overlap_parts not in (2, 3, 4):
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
         if latency_path is None:
@@ -728,8 +731,17 @@ class HipGPT2Engine:
             raise ValueError("prefill: token id out of range")
         pos_np = np.arange(R, dtype=np.int64) - np.repeat(ends - lens_np, lens_np)
         slot_np = np.repeat(np.asarray(slots, dtype=np.int64), lens_np)
+        if self._prefill_graph_ok(R, n):
+            return self._prefill_graphed(tok_np, pos_np, slot_np, ends - 1, np.asarray(slots), lens_np, penalty)
         tokens_d, pos_d, slot_d, last_d, slots_d, lens_d = (
             _to_device(a, dev) for a in (tok_np, pos_np, slot_np, ends - 1, np.asarray(slots), lens_np))
+        self._prefill_core(tokens_d, pos_d, slot_d, last_d, slots_d, lens_d, ops.AttnTiles(lens, dev), penalty)
+
+    def _prefill_core(self, tokens_d, pos_d, slot_d, last_d, slots_d, lens_d, tiles, penalty: float):
+        """Device side of a packed prefill (no host synchronisation: also captured as a graph)."""
+        cfg, dev = self.cfg, self.device
+        T = self.max_length
+        R, n = tokens_d.numel(), slots_d.numel()
         fin_d = (lens_d >= T).to(torch.int32)
         # per-sequence state scattered into the chosen slots on the device
         idx = slots_d.long()
@@ -755,8 +767,7 @@ class HipGPT2Engine:
         if self.w.fp8:
             h8 = torch.zeros(R, self.w.k_fp8, dtype=ops.FP8, device=dev)  # K padding stays zero
             hsc = torch.empty(R, dtype=f32, device=dev)
-        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None, h8=h8, hsc=hsc,
-                     tiles=ops.AttnTiles(lens, dev))
+        self._layers(x, parts, h, q, att, ff, slot_d, pos_d, pos_d + 1, R, final_h=None, h8=h8, hsc=hsc, tiles=tiles)
         hl = ops.layernorm_gather(x, last_d, self.w.lnf_g, self.w.lnf_b, cfg.layer_norm_epsilon)
         hsc_l = None
         if self.w.fp8:
@@ -765,6 +776,60 @@ class HipGPT2Engine:
             hl = hl8
         # first token: argmax rows are prompts (seen rows gathered), updates land in their slots
         self._lm_head_and_update(hl, n, penalty, seen=seen_d, hscale=hsc_l, slot_map=slots_d)
+
+    # hipGraph-replayed prefill, keyed by (packed rows, prompts): a (rows, prompts) shape seen
+    # twice is captured (inputs go through one static pinned -> device buffer, the tile table is
+    # padded by repeating its last tile); single-GPU engines only, small shapes only
+    PREFILL_GRAPH_MAX_ROWS = 4096
+    PREFILL_GRAPH_CACHE = 32
+
+    def _prefill_graph_ok(self, R: int, n: int) -> bool:
+        if not (self.use_graph and self.prefill_graphs and self.tp_size == 1 and R <= self.PREFILL_GRAPH_MAX_ROWS):
+            return False
+        key = (R, n)
+        if key in self._pgraphs:
+            return True
+        self._pseen[key] = self._pseen.get(key, 0) + 1
+        return self._pseen[key] >= 2 and len(self._pgraphs) < self.PREFILL_GRAPH_CACHE
+
+    def _prefill_graphed(self, tok, pos, slot, last, slots, lens, penalty: float):
+        R, n = tok.size, slots.size
+        key = (R, n)
+        TB = R // 16 + n  # >= the tile count of any R rows in n prompts
+        st = self._pgraphs.get(key)
+        if st is None:
+            words = 3 * R + 3 * n + 2 * TB
+            st = dict(host=torch.empty(words, dtype=torch.int32).pin_memory(),
+                      dev=torch.empty(words, dtype=torch.int32, device=self.device), copied=torch.cuda.Event(),
+                      graph=None, penalty=penalty)
+            self._pgraphs[key] = st
+        st["copied"].synchronize()  # the previous upload has left the staging buffer
+        hbuf = st["host"].numpy()
+        hbuf[:R], hbuf[R:2 * R], hbuf[2 * R:3 * R] = tok, pos, slot
+        o = 3 * R
+        hbuf[o:o + n], hbuf[o + n:o + 2 * n], hbuf[o + 2 * n:o + 3 * n] = last, slots, lens
+        nt = (lens + 15) // 16
+        seq = np.repeat(np.arange(n), nt)
+        k = np.arange(int(nt.sum())) - np.repeat(np.cumsum(nt) - nt, nt)
+        starts = np.cumsum(lens) - lens
+        tt = np.empty((TB, 2), dtype=np.int64)
+        tt[: len(seq), 0] = starts[seq] + 16 * k
+        tt[: len(seq), 1] = np.minimum(16, lens[seq] - 16 * k)
+        tt[len(seq):] = tt[len(seq) - 1]  # padding tiles repeat the last one (identical writes)
+        hbuf[o + 3 * n:] = tt.reshape(-1)
+        st["dev"].copy_(st["host"], non_blocking=True)
+        st["copied"].record()
+        if st["graph"] is None or st["penalty"] != penalty:
+            d = st["dev"]
+            tiles = ops.AttnTiles.__new__(ops.AttnTiles)
+            tiles.rows, tiles.n, tiles.t = R, TB, d[o + 3 * n:].view(TB, 2)
+            args = (d[:R], d[R:2 * R], d[2 * R:3 * R], d[o:o + n], d[o + n:o + 2 * n], d[o + 2 * n:o + 3 * n], tiles,
+                    penalty)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._prefill_core(*args)
+            st["graph"], st["penalty"] = g, penalty
+        st["graph"].replay()
 
     def _prefill(self, prompts: list[list[int]], B: int, penalty: float):
         """Static batch: prompts into slots [0, n), slots [n, B) inert."""

@@ -26,7 +26,6 @@ import grpc
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 from distributed_lms_raft_llm_amd import wire  # noqa: E402
 from distributed_lms_raft_llm_amd.lms.pdf import make_pdf  # noqa: E402

@@ -104,6 +104,36 @@ def test_graph_replay_equals_eager():
     assert a == b
 
 
+def test_prefill_graph_equals_eager():
+    """A (rows, prompts) prefill shape seen twice is replayed from a hipGraph (padded tile table):
+    tokens bit-identical to eager prefills, also for a different length mix of the same shape and
+    through the continuous-batching admit path."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    g_eng = HipGPT2Engine(cfg, w, max_batch=8, max_length=72)
+    e_eng = HipGPT2Engine(cfg, w, max_batch=8, max_length=72)
+    e_eng.prefill_graphs = False
+    mixes = [[32], [32], [32], [20, 12, 30], [30, 20, 12], [31, 1, 30], [40, 17]]
+    for i, lens in enumerate(mixes):
+        prompts = _prompts(cfg, lens, seed=10 + i)
+        assert g_eng.generate(prompts) == e_eng.generate(prompts), lens
+    assert (32, 1) in g_eng._pgraphs and g_eng._pgraphs[(32, 1)]["graph"] is not None
+    assert (62, 3) in g_eng._pgraphs and g_eng._pgraphs[(62, 3)]["graph"] is not None
+    assert not e_eng._pgraphs
+    # admit into arbitrary slots (the serving path), twice with one shape
+    for eng in (g_eng, e_eng):
+        eng._reset_slots(0, 8)
+    for rep in range(2):
+        prompts = _prompts(cfg, [9, 23], seed=30 + rep)
+        outs = []
+        for eng in (g_eng, e_eng):
+            eng.admit(prompts, [5, 2])
+            eng.decode(8, 6)
+            outs.append(eng.collect([5, 2]))
+        assert outs[0] == outs[1]
+
+
 @pytest.mark.parametrize("use_graph,parts,serial", [(True, 2, False), (False, 2, False), (True, 4, False),
                                                     (True, 2, True)])
 def test_overlapped_multi_stream_step_equals_serial(use_graph, parts, serial, monkeypatch):
