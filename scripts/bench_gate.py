@@ -7,7 +7,8 @@ fills the 512-token window.  Reports p50/p99 per-call latency and gate passes pe
 * ``batched``   -- the gate's batcher packs concurrent queries into one varlen encoder pass;
 * ``serial``    -- ``max_batch=1``: one encoder pass per query (what a per-request gate does).
 
-``--tutor echo`` isolates the LMS + gate path (the tutoring call is an in-process echo);
+Clients run in ``--client-procs`` separate processes (100 threads in the server's own interpreter
+would compete with it for the GIL); ``--tutor echo`` isolates the LMS + gate path (the tutoring call is an in-process echo);
 ``--tutor gpt2`` runs the real continuous-batching GPT-2 tutoring server on the same GPU.
 The reference's gate re-loads BERT from disk per query (~563 ms) on CPU.
 """
@@ -47,6 +48,39 @@ class EchoTutor:
         return pb.QueryResponse(success=True, response=f"Question: {request.query}\nAnswer: synthetic")
 
 
+def _client_proc(conn):
+    """Client worker process (spawned before the parent touches the GPU): on each request
+    (addr, [(token, query)]) fire all calls at once from threads, reply with latencies (ms)."""
+    import grpc as _grpc  # noqa: F401  (fresh interpreter: import here)
+
+    from distributed_lms_raft_llm_amd import wire as _wire
+    from distributed_lms_raft_llm_amd.wire import pb as _pb
+
+    stub = None
+    while True:
+        msg = conn.recv()
+        if msg is None:
+            return
+        addr, calls = msg
+        if stub is None:
+            stub = _wire.Stub("LMS", _wire.channel(addr))
+        lat = [0.0] * len(calls)
+        barrier = threading.Barrier(len(calls))
+
+        def one(i):
+            barrier.wait()
+            t = time.perf_counter()
+            r = stub.GetLLMAnswer(_pb.QueryRequest(token=calls[i][0], query=calls[i][1]), timeout=120)
+            lat[i] = (time.perf_counter() - t) * 1e3 if (r.success and r.response) else -1.0
+
+        ths = [threading.Thread(target=one, args=(i,)) for i in range(len(calls))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        conn.send(lat)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=100)
@@ -57,7 +91,20 @@ def main():
     ap.add_argument("--window-ms", type=float, default=1.0)
     ap.add_argument("--max-batch", type=int, default=64)
     ap.add_argument("--device", default="cuda", help="'cpu' = torch reference encoder (dry run)")
+    ap.add_argument("--client-procs", type=int, default=4,
+                    help="client processes (0 = client threads inside the server process)")
     args = ap.parse_args()
+
+    # client processes first: spawned before this process initialises the GPU
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    clients = []
+    for _ in range(args.client_procs):
+        a, b = ctx.Pipe()
+        p = ctx.Process(target=_client_proc, args=(b,), daemon=True)
+        p.start()
+        clients.append((p, a))
 
     import torch
 
@@ -98,6 +145,14 @@ def main():
     queries = [" ".join(rng.choice(WORDS) for _ in range(rng.randint(4, 40))) for _ in range(args.clients)]
 
     def burst():
+        if clients:  # fan the calls out over the client processes, all at once
+            shares = [[(tokens[i], queries[i]) for i in range(k, args.clients, len(clients))]
+                      for k in range(len(clients))]
+            for (_, conn), calls in zip(clients, shares):
+                conn.send((addr, calls))
+            lat = [x for _, conn in clients for x in conn.recv()]
+            assert min(lat) >= 0, "a call failed"
+            return lat
         lat = [0.0] * args.clients
         barrier = threading.Barrier(args.clients)
 
@@ -128,12 +183,15 @@ def main():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         print(json.dumps({"bench": "gate_concurrency", "mode": mode, "tutor": args.tutor, "clients": args.clients,
+                          "client_procs": args.client_procs,
                           "rounds": args.rounds, "gate_model": args.gate_model,
                           "p50_ms": round(statistics.median(lat), 2), "p99_ms": round(pct(lat, 0.99), 2),
                           "max_ms": round(max(lat), 2), "calls_per_s": round(len(lat) / wall, 1),
                           "gate_passes": gate.passes - p0,
                           "queries_per_pass": round((gate.batched_queries - q0) / max(1, gate.passes - p0), 2)}),
               flush=True)
+    for _, conn in clients:
+        conn.send(None)
     srv.stop(grace=0)
     if tserver is not None:
         tserver.stop()
