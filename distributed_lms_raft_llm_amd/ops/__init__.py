@@ -67,14 +67,33 @@ def build(force: bool = False, verbose: bool = False, checked: bool = False) -> 
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = path.with_suffix(f".so.tmp{os.getpid()}")
-    cmd = [hipcc, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
-           "-Wno-unused-result"] + (["-DDLMS_DEVICE_CHECKS=1"] if checked else []) + ["-o", str(tmp)] + \
-        [str(s) for s in _sources()]
-    if verbose:
-        print(" ".join(cmd))
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+    flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wno-unused-result"] + \
+        (["-DDLMS_DEVICE_CHECKS=1"] if checked else [])
+    # one hipcc per translation unit, in parallel (the kernels of a unit never call another
+    # unit's device code, so no relocatable device code is needed), then one link
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
+    jobs = max(1, min(len(_sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with tempfile.TemporaryDirectory(prefix="dlms_build_") as td:
+        objs = [os.path.join(td, src.stem + ".o") for src in _sources()]
+
+        def compile_one(i):
+            cmd = [hipcc] + flags + ["-c", str(_sources()[i]), "-o", objs[i]]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            return subprocess.run(cmd, capture_output=True, text=True)
+
+        with ThreadPoolExecutor(jobs) as ex:
+            for src, res in zip(_sources(), ex.map(compile_one, range(len(objs)))):
+                if res.returncode != 0:
+                    raise RuntimeError(f"hipcc failed on {src.name} ({res.returncode}):\n{res.stderr[-4000:]}")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", str(tmp)] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-4000:]}")
     os.replace(tmp, path)
     return path
 
