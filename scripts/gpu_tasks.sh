@@ -15,6 +15,7 @@
 #   trace:<tag>      per-dispatch kernel trace of one B=1024 generation (timeline analysis) -> gpurun_out/trace_<tag>/
 #   skinny           latency-path kernel microbench                -> gpurun_out/skinny.jsonl
 #   attn             split-K flash-decode sweep (B x T x waves x workgroups)   -> gpurun_out/attn.jsonl
+#   pgemm            packed-prefill GEMMs (32768 rows) vs hipBLASLt -> gpurun_out/pgemm.jsonl
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
@@ -78,6 +79,7 @@ for task in "$@"; do
             gzip -f "$f"; cat gpurun_out/trace_$tag/timeline.txt ;;
         skinny) step 300 gpurun_out/skinny.jsonl python -u scripts/bench_skinny.py ;;
         attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
+        pgemm) step 300 gpurun_out/pgemm.jsonl python -u scripts/bench_prefill_gemm.py; grep '^{' gpurun_out/pgemm.jsonl ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
         gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;
         serving) step 400 gpurun_out/serving.jsonl python -u scripts/bench_serving.py --rates 20,200,1000 --queries 400 \
