@@ -73,6 +73,7 @@ class _Req:
     future: Future
     t_submit: float = field(default_factory=time.perf_counter)
     t_first: float = 0.0
+    steps_left: int = 0  # decode steps until max_length (an upper bound: EOS may come first)
 
 
 class ContinuousBatcher:
@@ -174,18 +175,29 @@ class ContinuousBatcher:
                 for s, r in admits:
                     self._active[s] = r
                     r.t_first = t_first
+                    r.steps_left = max(0, eng.max_length - len(r.prompt) - 1)  # prefill made token 1
                     METRICS.observe(f"{self.name}_queue_ms", (ta - r.t_submit) * 1e3)
                     METRICS.observe(f"{self.name}_ttft_ms", (t_first - r.t_submit) * 1e3)
             cur = None
+            # never decode far past the point where every live sequence has hit max_length: the last
+            # chunk is cut to the longest remaining budget, and once every budget is spent only a
+            # single step runs while the in-flight flags retire them (one step, not a whole no-op
+            # chunk, on every query's latency at low load; at least one step keeps the loop making
+            # progress even if a sequence's flag were late)
+            steps = 0
             if self._active:
+                steps = max(1, min(self.chunk, max(r.steps_left for r in self._active.values())))
+            if steps > 0:
                 B = min(_bucket(max(self._active) + 1), eng.max_batch)
                 td = time.perf_counter()
                 with roctx_range("decode_chunk"):
-                    eng.decode(B, self.chunk, self.penalty)
+                    eng.decode(B, steps, self.penalty)
                     cur = (flags_async(eng, B), dict(self._active), health_async(eng))
-                self.steps += self.chunk
+                for r in self._active.values():
+                    r.steps_left = max(0, r.steps_left - steps)
+                self.steps += steps
                 TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
-                                steps=self.chunk)
+                                steps=steps)
             if retiring is not None:  # gathered behind the chunk before `cur`: ready or nearly
                 self._retire(*retiring)
                 retiring = None
