@@ -230,6 +230,16 @@ class HipGPT2Engine:
                 if lw.w_qkv_sh is None:
                     lw.w_qkv_sh = ops.shuffle_weight(lw.w_qkv)
                     lw.w_fc_sh = ops.shuffle_weight(lw.w_fc)
+        # latency path, TP=1: out-proj / c_proj as skinny MFMA GEMMs adding into the residual in
+        # place (pre-shuffled W_o / W_proj copies)
+        self.small_inplace = (self.small_max > 0 and self.tp_size == 1 and
+                              os.environ.get("DLMS_SMALL_INPLACE", "1") != "0")
+        if self.small_inplace:
+            for lw in self.w.layers:
+                if lw.w_p_sh is None:
+                    lw.w_p_sh = ops.shuffle_weight(lw.w_p)
+                if lw.w_o_sh is None:
+                    lw.w_o_sh = ops.shuffle_weight(lw.w_o)
         # attention fused with the out-projection for <= 4 rows (one launch fewer per layer); its
         # workgroups recompute a head's attention, so only for short caches
         # (TP=1: its per-head slabs are summed by the next fused add+LN kernel, 12 or 16 of them)
@@ -616,6 +626,9 @@ class HipGPT2Engine:
         tp = self.tp_size > 1
         split = 1 if tp else self.SMALL_SPLIT
         parts = self.parts[:, :B]
+        # TP=1: the row-parallel projections add straight into the residual (skinny MFMA, column-
+        # owning, x += a W^T + b in place: no split-K slabs for the next kernel to sum)
+        inplace = not tp and self.small_inplace
 
         def row_parallel(a, w):
             ops.gemm(a, w, ops.EPI_PARTIAL, out=self.parts, split_k=split)
@@ -635,17 +648,32 @@ class HipGPT2Engine:
                 cur = 1 - cur
             if self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
                 ops.attention_oproj(self.q[:B], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts)
-                mlp_parts, ns = self.ao_parts[:, :B], self.w.n_heads_local
+                mlp_parts, ns, rb = self.ao_parts[:, :B], self.w.n_heads_local, lw.b_o
+            elif inplace:
+                self._attn(r, li)
+                ops.skinny_gemm(self.att[:B], lw.w_o_sh, ops.EPI_F32, bias=lw.b_o, out=bufs[cur])
+                mlp_parts, ns, rb = None, 0, None
             else:
                 self._attn(r, li)
-                mlp_parts, ns = parts, row_parallel(r.att, lw.w_o)
-            ops.skinny_addln_gemm(bufs[cur], lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps,
-                                  x_out=bufs[1 - cur], parts=mlp_parts, nsplit=ns, res_bias=lw.b_o, bias=lw.b_fc,
-                                  out=r.ff)
-            cur = 1 - cur
-            pend = (row_parallel(r.ff, lw.w_p), lw.b_p)
-        ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, parts=self.parts, nsplit=pend[0], bias=pend[1],
-                          out_bf16=self.h[:B])
+                mlp_parts, ns, rb = parts, row_parallel(r.att, lw.w_o), lw.b_o
+            if ns:
+                ops.skinny_addln_gemm(bufs[cur], lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps,
+                                      x_out=bufs[1 - cur], parts=mlp_parts, nsplit=ns, res_bias=rb, bias=lw.b_fc,
+                                      out=r.ff)
+                cur = 1 - cur
+            else:  # residual already complete: LN2 only
+                ops.skinny_addln_gemm(bufs[cur], lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps,
+                                      bias=lw.b_fc, out=r.ff)
+            if inplace:
+                ops.skinny_gemm(self.ff[:B], lw.w_p_sh, ops.EPI_F32, bias=lw.b_p, out=bufs[cur])
+                pend = None
+            else:
+                pend = (row_parallel(r.ff, lw.w_p), lw.b_p)
+        if pend is None:
+            ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, out_bf16=self.h[:B])
+        else:
+            ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, parts=self.parts, nsplit=pend[0],
+                              bias=pend[1], out_bf16=self.h[:B])
         self._lm_head_and_update(self.h[:B], B, penalty)
 
     def _decode_step(self, B: int, penalty: float):

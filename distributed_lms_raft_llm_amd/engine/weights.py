@@ -58,7 +58,8 @@ class LayerWeights:
     # skinny kernels; filled by the engine when that path is enabled
     w_qkv_sh: torch.Tensor | None = None
     w_fc_sh: torch.Tensor | None = None
-    w_o_sh: torch.Tensor | None = None  # fused attention + out-projection (B <= 4)
+    w_o_sh: torch.Tensor | None = None  # fused attention + out-projection / in-place out-proj
+    w_p_sh: torch.Tensor | None = None  # in-place c_proj (latency path, TP=1)
 
 
 @dataclass

@@ -78,6 +78,8 @@ for task in "$@"; do
             step 120 gpurun_out/trace_$tag/timeline.txt python scripts/timeline.py "$f"
             gzip -f "$f"; cat gpurun_out/trace_$tag/timeline.txt ;;
         skinny) step 300 gpurun_out/skinny.jsonl python -u scripts/bench_skinny.py ;;
+        skinnyhot) step 300 gpurun_out/skinny_hot.jsonl python -u scripts/bench_skinny.py --batches 1 --cold-mb 1 --T 150
+                   step 300 gpurun_out/skinny_cold.jsonl python -u scripts/bench_skinny.py --batches 1 --cold-mb 512 --T 150 ;;
         attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
         pgemm) step 300 gpurun_out/pgemm.jsonl python -u scripts/bench_prefill_gemm.py; grep '^{' gpurun_out/pgemm.jsonl ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
