@@ -133,9 +133,10 @@ class HipGPT2Engine:
     # (row, head) pairs up to which decode attention uses the split-K kernel (profiles/r2_skinny_bench.log:
     # at 32 rows x 12 heads, T=150: 7.9 us vs 12.3 us for one wave per pair)
     SPLIT_ATTN_MAX_PAIRS = 1024
-    # fused attention + out-projection up to this many rows: batch 1 40.6 vs 43.3 ms per query,
-    # batch 4 48.0 vs 47.3 (its workgroups recompute a head's attention per row)
-    FUSE_AO_MAX_ROWS = 2
+    # fused attention + out-projection up to this many rows (its workgroups recompute a head's
+    # attention per row): against the split attention + in-place skinny out-projection, batch 1
+    # 36.8 vs 37.9 ms per query, batch 2 39.2 vs 38.7 (profiles/r2_attn_oproj_ab.txt)
+    FUSE_AO_MAX_ROWS = 1
     # split-K of the row-parallel projections on the latency path (fixed: the fused add+LN
     # kernel sums exactly this many slabs)
     SMALL_SPLIT = 4

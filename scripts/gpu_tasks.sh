@@ -21,6 +21,7 @@
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
 #   e2e:<n>          scripts/run_config.py --config n (Raft cluster + gate + tutor) -> gpurun_out/e2e_<n>.log
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
+#   sweep1:<...>     the same at batch 1 and 2 (p50 per query)     -> gpurun_out/sweep1.jsonl
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 180 --timeout-method thread"
@@ -95,6 +96,15 @@ for task in "$@"; do
                 echo "{\"env\": \"$envs\", \"bench\": $(grep '^{' gpurun_out/sweep.log | tail -1)}" >> gpurun_out/sweep.jsonl
                 tail -1 gpurun_out/sweep.jsonl
             done ;;
+        sweep1:*)  # the same at batch 1 and 2 (latency path): value = tok/s, plus p50 per query
+            IFS=';' read -ra sets <<< "${task#sweep1:}"
+            for envs in "${sets[@]}"; do
+                for b in 1 2; do
+                    step 300 gpurun_out/sweep1.log env ${envs//,/ } python -u bench.py --batch $b --steps 8 --warmup 2 --latency-batches ""
+                    echo "{\"env\": \"$envs\", \"batch\": $b, \"bench\": $(grep '^{' gpurun_out/sweep1.log | tail -1)}" >> gpurun_out/sweep1.jsonl
+                done
+            done
+            python -c "import json; [print(d['env'], d['batch'], d['bench']['p50_query_latency_ms']) for d in map(json.loads, open('gpurun_out/sweep1.jsonl'))]" ;;
         *) echo "unknown task $task" >&2; exit 2 ;;
     esac
 done
