@@ -258,6 +258,13 @@ class HipGPT2Engine:
                 if lw.w_o_sh is None:
                     lw.w_o_sh = ops.shuffle_weight(lw.w_o)
             self.ao_parts = torch.zeros(self.w.n_heads_local, 4, cfg.n_embd, dtype=torch.float32, device=self.device)
+        # batch 1: head groups of H/4 (3 or 4 heads) -> 4 slabs (DLMS_AO_GROUPS=0: one slab per head)
+        Hl = self.w.n_heads_local
+        self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4) and
+                                      os.environ.get("DLMS_AO_GROUPS", "1") != "0") else 0
+        self.ao_group_tiles = int(os.environ.get("DLMS_AO_GROUP_TILES", "3"))
+        if self.ao_groups and (cfg.n_embd // 16) % self.ao_group_tiles:
+            self.ao_group_tiles = 1
         # LM head of the throughput path (>= PS_LM_MIN_ROWS rows): panel-resident gemm_ps on a
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
@@ -647,7 +654,12 @@ class HipGPT2Engine:
                                       parts=parts, nsplit=pend[0], res_bias=pend[1], bias=lw.b_qkv, q_out=r.q,
                                       k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
                 cur = 1 - cur
-            if self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
+            if self.fuse_ao and B == 1 and self.ao_groups:
+                # heads in groups of H/4: exactly the 4 slabs the fused add+LN sums cheaply
+                ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
+                                            self.ao_groups, tiles=self.ao_group_tiles)
+                mlp_parts, ns, rb = self.ao_parts[:4, :1], 4, lw.b_o
+            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
                 ops.attention_oproj(self.q[:B], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts)
                 mlp_parts, ns, rb = self.ao_parts[:, :B], self.w.n_heads_local, lw.b_o
             elif inplace:

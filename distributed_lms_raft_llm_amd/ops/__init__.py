@@ -150,6 +150,7 @@ def _bind(L):
         "dlms_skinny_gemm": [I, P, I, P, P, F, P, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_attention_split": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, I, P, P, I, P],
         "dlms_attention_oproj": [P, I, P, P, P, P, I, I, I, I, F, P, I, I, P, I, ctypes.c_longlong, P],
+        "dlms_attention_oproj_grouped": [P, P, P, P, P, I, I, I, I, F, P, I, I, P, ctypes.c_longlong, P],
         "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
                                    ctypes.POINTER(GemmEpi), P],
         "dlms_skinny_addln_max_rows": [I],
@@ -1004,6 +1005,37 @@ def attention_oproj(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                                       H, T, S, float(sc), _p(wo_sh), N, int(nt), _p(parts), parts.stride(1),
                                       parts.stride(0), _stream()),
            "attention_oproj")
+    return parts
+
+
+def attention_oproj_grouped(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
+                            row_kvlen: torch.Tensor, wo_sh: torch.Tensor, parts: torch.Tensor, heads_per_group: int,
+                            scale: float | None = None, tiles: int = 3) -> torch.Tensor:
+    """``attention_oproj`` for ONE row with heads in groups of ``heads_per_group`` (3 or 4): group g's
+    share of the out-projection goes to ``parts[g, 0, :N]`` -- H / heads_per_group slabs."""
+    _req(q, torch.bfloat16, "q", 2)
+    _req(k_cache, torch.bfloat16, "k_cache", 4)
+    _req(v_cache, torch.bfloat16, "v_cache", 4)
+    _req(row_slot, torch.int32, "row_slot", 1)
+    _req(row_kvlen, torch.int32, "row_kvlen", 1)
+    _req(wo_sh, torch.bfloat16, "wo_sh", 4)
+    _req(parts, torch.float32, "parts", 3)
+    S, H, T, hd = k_cache.shape
+    N = wo_sh.shape[0] * 16
+    hg = int(heads_per_group)
+    if q.shape[0] != 1:
+        raise ValueError("attention_oproj_grouped: one row")
+    if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64 or wo_sh.shape[1] * 32 != H * 64:
+        raise ValueError("attention_oproj_grouped: bad shapes")
+    if hg not in (3, 4) or H % hg or (N // 16) % tiles:
+        raise ValueError("attention_oproj_grouped: heads_per_group in {3, 4} dividing H, tiles dividing N/16")
+    if parts.shape[0] < H // hg or parts.shape[2] < N or parts.stride(2) != 1:
+        raise ValueError("attention_oproj_grouped: parts must be [>= H/hg, >= 1, >= N]")
+    sc = (1.0 / 8.0) if scale is None else scale
+    _check(lib().dlms_attention_oproj_grouped(_p(q), _p(k_cache), _p(v_cache), _p(row_slot), _p(row_kvlen), H, hg, T,
+                                              S, float(sc), _p(wo_sh), N, int(tiles), _p(parts), parts.stride(0),
+                                              _stream()),
+           "attention_oproj_grouped")
     return parts
 
 

@@ -932,6 +932,164 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(
     }
 }
 
+// Head-grouped variant for ONE row (batch 1): workgroup (g, j) covers HG heads with 4 waves per
+// head (keys split 4 ways, log-sum-exp merge in LDS) and their 2*HG k-blocks of its NT W_o tiles,
+// so the out-projection lands in H / HG slabs instead of H -- with HG = H / 4 exactly the four
+// split-K slabs the fused add+LN kernel already sums (12 slabs cost that kernel ~2 us at batch 1).
+template <int HG, int NT>
+__global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ row_slot, const int* __restrict__ row_kvlen, int H, int t_max, int n_slots,
+    float scale_log2, const bf16_t* __restrict__ Wo_sh, int N, float* __restrict__ part, long long split_stride) {
+    constexpr int NW = 4 * HG;
+    constexpr int U = HG >= 4 ? 4 : 8;  // 16 waves per CU leave 128 VGPRs per lane
+    constexpr int AW = HG * 64 + 8;  // A image row (bf16), padded
+    __shared__ float part_s[NW][8][10];
+    __shared__ __attribute__((aligned(16))) bf16_t aimg[16][AW];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int grp = blockIdx.x;
+    const int j = blockIdx.y;
+    const int nkb = (H * 64) >> 5;
+    const int fr = lane & 15, gg = lane >> 4;
+
+    // (0) W_o fragments: wave t < NT owns output tile j*NT + t, k-blocks of the group's heads
+    bf16x8_t wb[2 * HG];
+    if (wave < NT) {
+        const bf16x8_t* src =
+            reinterpret_cast<const bf16x8_t*>(Wo_sh) + ((size_t)(j * NT + wave) * nkb + 2 * HG * grp) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < 2 * HG; ++k) wb[k] = src[k * 64];
+    }
+
+    // (1) attention: wave w -> head grp*HG + w/4, key slice w%4
+    const int hh = wave >> 2, sl = wave & 3;
+    const int h = grp * HG + hh;
+    const int g = lane >> 3, c = lane & 7;
+    const int slot = (int)dlms_idx(row_slot[0], n_slots, CHK_ATTN_SLOT);
+    int kvlen = row_kvlen[0];
+    kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
+    const int span = ((kvlen + 3) / 4 + 7) & ~7;
+    const int t_lo = sl * span < kvlen ? sl * span : kvlen;
+    const int t_hi = t_lo + span < kvlen ? t_lo + span : kvlen;
+    const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
+    const bf16_t* K = kc + head_off + c * 8;
+    const bf16_t* V = vc + head_off + c * 8;
+    float qf[8];
+    unpack8(*reinterpret_cast<const uint4*>(q + h * 64 + c * 8), qf);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qf[e] *= scale_log2;
+    float m = -INFINITY, l = 0.f;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t0 = t_lo; t0 < t_hi; t0 += 8 * U) {
+        uint4 kr[U], vr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int t = t0 + u * 8 + g;
+            t = t < t_hi ? t : t_hi - 1;
+            kr[u] = *reinterpret_cast<const uint4*>(K + (size_t)t * 64);
+            vr[u] = *reinterpret_cast<const uint4*>(V + (size_t)t * 64);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float kf[8];
+            unpack8(kr[u], kf);
+            float sc = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sc += qf[e] * kf[e];
+            sc += __shfl_xor(sc, 1, 64);
+            sc += __shfl_xor(sc, 2, 64);
+            sc += __shfl_xor(sc, 4, 64);
+            if (t0 + u * 8 + g < t_hi) {
+                const float m_new = fmaxf(m, sc);
+                const float corr = exp2f(m - m_new);
+                const float p = exp2f(sc - m_new);
+                float vf[8];
+                unpack8(vr[u], vf);
+                l = l * corr + p;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] = acc[e] * corr + p * vf[e];
+                m = m_new;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+        const float m_o = __shfl_xor(m, o, 64);
+        const float l_o = __shfl_xor(l, o, 64);
+        const float m_n = fmaxf(m, m_o);
+        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
+        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
+        l = l * a + l_o * b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + __shfl_xor(acc[e], o, 64) * b;
+        m = m_n;
+    }
+    if (g == 0) {
+        part_s[wave][c][0] = m;
+        part_s[wave][c][1] = l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part_s[wave][c][2 + e] = acc[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < 16 * 8 * HG) {  // (row r, head hh2, chunk cc) -> A image (row 0 real, rows 1..15 zero)
+        const int r = threadIdx.x / (8 * HG);
+        const int hh2 = (threadIdx.x / 8) % HG, cc = threadIdx.x & 7;
+        float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (r == 0) {
+            float M_ = -INFINITY;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) M_ = fmaxf(M_, part_s[hh2 * 4 + w][cc][0]);
+            float L = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float mw = part_s[hh2 * 4 + w][cc][0];
+                if (mw == -INFINITY) continue;
+                const float f = exp2f(mw - M_);
+                L += part_s[hh2 * 4 + w][cc][1] * f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o8[e] += part_s[hh2 * 4 + w][cc][2 + e] * f;
+            }
+            const float inv = 1.f / L;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o8[e] *= inv;
+        }
+        *reinterpret_cast<uint4*>(&aimg[r][hh2 * 64 + cc * 8]) = pack8(o8);
+    }
+    __syncthreads();
+
+    // (2) o[16 x HG*64] . W_o[tile, group k-blocks]^T -> slab grp (row 0 only)
+    if (wave >= NT) return;
+    f32x4_t d = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 2 * HG; ++k) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&aimg[fr][k * 32 + gg * 8]);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[k], d, 0, 0, 0);
+    }
+    if (gg == 0) part[(size_t)grp * split_stride + (j * NT + wave) * 16 + fr] = d[0];  // row 0 of the tile
+}
+
+extern "C" hipError_t dlms_attention_oproj_grouped(const void* q, const void* kc, const void* vc, const int* row_slot,
+                                                   const int* row_kvlen, int H, int hg, int t_max, int n_slots,
+                                                   float scale, const void* wo_sh, int N, int nt, float* part,
+                                                   long long split_stride, hipStream_t stream) {
+    if (H < 1 || hg < 1 || H % hg || t_max < 1 || N % 16 || nt < 1 || nt > 4 * hg || (N / 16) % nt)
+        return hipErrorInvalidValue;
+    const float sl2 = scale * 1.4426950408889634f;
+    const dim3 grid(H / hg, (N / 16) / nt);
+    auto go = [&](auto kern, int threads) {
+        hipLaunchKernelGGL(kern, grid, dim3(threads), 0, stream, reinterpret_cast<const bf16_t*>(q),
+                           reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
+                           row_kvlen, H, t_max, n_slots, sl2, reinterpret_cast<const bf16_t*>(wo_sh), N, part,
+                           split_stride);
+    };
+#define AOG(HG_, NT_) \
+    if (hg == HG_ && nt == NT_) { go(attn_oproj_hg_kernel<HG_, NT_>, 256 * HG_); return hipGetLastError(); }
+    AOG(3, 1) AOG(3, 2) AOG(3, 3) AOG(3, 4) AOG(4, 1) AOG(4, 2) AOG(4, 3) AOG(4, 4)
+#undef AOG
+    return hipErrorInvalidValue;
+}
+
 extern "C" hipError_t dlms_attention_oproj(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                            const int* row_kvlen, int M, int H, int t_max, int n_slots, float scale,
                                            const void* wo_sh, int N, int nt, float* part, int ldp,

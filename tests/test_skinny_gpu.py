@@ -224,6 +224,26 @@ def test_attention_oproj(M, H, T):
     assert torch.all(parts[:, M:] == 7.0)  # rows >= M untouched
 
 
+@pytest.mark.parametrize("H,hg,tiles", [(12, 3, 3), (12, 3, 1), (16, 4, 4), (16, 4, 2), (12, 4, 3)])
+@pytest.mark.parametrize("T", [1, 37, 150])
+def test_attention_oproj_grouped(H, hg, tiles, T):
+    """One row, heads in groups of hg: slab g == sum over its heads of attn_h(q) -> bf16 -> @ W_o[:, h]^T."""
+    ops = _ops()
+    N, S = H * 64, 5
+    kc, vc = _rand(S, H, T, 64, seed=121), _rand(S, H, T, 64, seed=122)
+    q = _rand(1, H * 64, seed=123)
+    wo = _rand(N, H * 64, scale=0.05, seed=124)
+    slot = torch.tensor([3], dtype=torch.int32, device=DEV)
+    kvlen = torch.tensor([T], dtype=torch.int32, device=DEV)
+    parts = torch.full((H // hg, 2, N), 7.0, device=DEV)
+    ops.attention_oproj_grouped(q, kc, vc, slot, kvlen, ops.shuffle_weight(wo), parts, hg, tiles=tiles)
+    o = _attn_ref(q, kc, vc, slot, kvlen).to(torch.bfloat16).float().reshape(H, 64)
+    for g in range(H // hg):
+        ref = sum(o[h] @ wo.float()[:, 64 * h:64 * h + 64].t() for h in range(g * hg, g * hg + hg))
+        torch.testing.assert_close(parts[g, 0], ref, atol=3e-2, rtol=2e-2)
+    assert torch.all(parts[:, 1] == 7.0)
+
+
 @pytest.mark.parametrize("ns", [12, 16])
 def test_skinny_addln_many_slabs(ns):
     """The fused add+LN consumes 12 / 16 per-head slabs (fixed order) like 4."""
