@@ -215,6 +215,10 @@ class HipGPT2Engine:
         # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
         self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "0"))
         self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
+        # latency path, TP=1: ln_f fused into a skinny LM head (one kernel fewer per token) -- opt-in:
+        # the skinny LM head is slower than the tiled one by more than the launch it saves
+        # (batch 1: 37.3 vs 35.9 ms per query, profiles/r2_lm_head_b1.txt)
+        self.lm_ln_fused = os.environ.get("DLMS_LM_LN_FUSED", "0") == "1"
         self.alt_attn = os.environ.get("DLMS_OVERLAP_ALT_ATTN", "0") == "1"
         self.prefill_graphs = os.environ.get("DLMS_PREFILL_GRAPH", "1") != "0"
         self._pgraphs: dict[tuple[int, int], dict] = {}
@@ -270,7 +274,7 @@ class HipGPT2Engine:
         # (profiles/r2_gemm_ps_vs_tiled.log)
         self.lm_head_sh = None
         ps_lm = self.max_batch >= self.PS_LM_MIN_ROWS and os.environ.get("DLMS_PS_LMHEAD", "1") != "0"
-        if not self.w.fp8 and (ps_lm or (self.small_max > 0 and self.lm_skinny)):
+        if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
             # (the latency path's skinny LM head reads the same pre-shuffled copy)
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
         self._side_streams: list[torch.cuda.Stream] = []
@@ -471,15 +475,18 @@ class HipGPT2Engine:
             self._attn_out_mlp(r, li)
         self._final_ln(r, final_h)
 
-    def _lm_head_and_update(self, hidden: torch.Tensor, B: int, penalty: float, seen: torch.Tensor | None = None,
-                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0):
+    def _lm_head_and_update(self, hidden: torch.Tensor | None, B: int, penalty: float, seen: torch.Tensor | None = None,
+                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0,
+                            keys_ready: bool = False):
         """LM head with the fused penalty + argmax on ``hidden`` (bf16, or e4m3 with ``hscale``),
         then the greedy bookkeeping.  Rows map to slots [lo, lo + B) or through ``slot_map``."""
         cfg = self.cfg
         hi = lo + B
         seen_rows = self.seen[lo:hi] if seen is None else seen
         P = self.key_parts.shape[1]  # partial keys per row the LM head writes (and the consumer reads)
-        if hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B >= self.PS_LM_MIN_ROWS and \
+        if keys_ready:  # the caller ran the LM head (skinny, ln_f fused): one key per 64 columns
+            P = self.lm_head_sh.shape[0] * 16 // 64
+        elif hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B >= self.PS_LM_MIN_ROWS and \
                 self.max_batch >= self.PS_LM_MIN_ROWS:
             P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16)
             ops.gemm_ps(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
@@ -682,6 +689,13 @@ class HipGPT2Engine:
                 pend = None
             else:
                 pend = (row_parallel(r.ff, lw.w_p), lw.b_p)
+        if pend is None and self.lm_ln_fused:
+            # ln_f in the LM head's prologue: every workgroup normalises the (few) rows itself
+            ops.skinny_gemm(bufs[cur], self.lm_head_sh, ops.EPI_ARGMAX, ln=(self.w.lnf_g, self.w.lnf_b, eps),
+                            argmax_out=self.key_parts[:B], seen=self.seen[:B], vocab=self.cfg.vocab_size,
+                            col_offset=self.w.vocab_range[0], penalty=penalty)
+            self._lm_head_and_update(None, B, penalty, keys_ready=True)
+            return
         if pend is None:
             ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, out_bf16=self.h[:B])
         else:

@@ -715,7 +715,8 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
     """Decode GEMM for M <= 32 rows against a ``shuffle_weight`` weight ([N/16, K/32, 64, 8]).
 
     ``ln=(gamma, beta, eps)``: ``a`` is the f32 residual x [M, K] and the kernel LayerNorms it in
-    its prologue (EPI_BF16 / EPI_GELU_TANH / EPI_QKV); otherwise ``a`` is bf16 [M, K].
+    its prologue (EPI_BF16 / EPI_GELU_TANH / EPI_QKV / EPI_ARGMAX: ln_f fused into the LM head);
+    otherwise ``a`` is bf16 [M, K].
     EPI_F32 adds ``acc + bias`` into ``out`` (f32 [M, N], in place: the residual stream);
     EPI_PARTIAL stores the raw f32 partial (TP); EPI_ARGMAX writes one key per (row, 64 columns)
     into ``argmax_out`` [M, >= N/64] exactly like ``gemm(..., EPI_ARGMAX)``."""
@@ -731,8 +732,8 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
         _req(b_, torch.float32, "ln beta", 1)
         if g_.numel() != K or b_.numel() != K or K > 2048 or K % 4:
             raise ValueError("skinny_gemm: LN params must match K (<= 2048)")
-        if epi not in (EPI_BF16, EPI_GELU_TANH, EPI_QKV):
-            raise ValueError("skinny_gemm: the LayerNorm prologue feeds bf16 / GELU / QKV epilogues only")
+        if epi not in (EPI_BF16, EPI_GELU_TANH, EPI_QKV, EPI_ARGMAX):
+            raise ValueError("skinny_gemm: the LayerNorm prologue feeds bf16 / GELU / QKV / argmax epilogues only")
     else:
         _req(a, torch.bfloat16, "a", 2)
         if epi in (EPI_GELU_TANH, EPI_QKV):

@@ -351,7 +351,9 @@ extern "C" hipError_t dlms_skinny_gemm(int epi, const void* A, int lda, const fl
         SK_LN(SK_GELU_TANH)
         SK_LN(SK_QKV)
         SK_NOLN(SK_F32)
-        SK_NOLN(SK_ARGMAX)
+        case SK_ARGMAX:  // with the LN prologue: ln_f fused into the latency path's LM head
+            return ln ? skinny_mt<SK_ARGMAX, true>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream)
+                      : skinny_mt<SK_ARGMAX, false>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream);
         SK_NOLN(SK_PARTIAL)
         default: return hipErrorInvalidValue;
     }

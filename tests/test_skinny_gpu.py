@@ -136,6 +136,29 @@ def test_skinny_argmax_penalty(M):
     assert torch.equal(idx[clear].cpu(), top2.indices[clear, 0].cpu())
 
 
+@pytest.mark.parametrize("M", [1, 5])
+def test_skinny_argmax_with_ln_prologue(M):
+    """ln_f fused into the skinny LM head: keys == those of the bf16 LN output fed to the same kernel."""
+    ops = _ops()
+    V, K = 3000, 768
+    Vp = (V + 63) // 64 * 64
+    x = _rand(M, K, seed=131, dtype=torch.float32) * 2 + 0.3
+    g, b = _rand(K, seed=132, dtype=torch.float32), _rand(K, seed=133, dtype=torch.float32)
+    w_sh = ops.shuffle_weight(_rand(Vp, K, scale=0.05, seed=134))
+    seen = torch.zeros(M, Vp // 32, dtype=torch.int32, device=DEV)
+    seen[:, 3] = 0x0F0F0F0F
+    k1 = torch.zeros(M, Vp // 64, dtype=torch.int64, device=DEV)
+    k2 = torch.zeros_like(k1)
+    ops.skinny_gemm(x, w_sh, ops.EPI_ARGMAX, ln=(g, b, 1e-5), argmax_out=k1, seen=seen, vocab=V, penalty=1.2)
+    h = _ln_ref(x, g, b, 1e-5).to(torch.bfloat16)
+    ops.skinny_gemm(h, w_sh, ops.EPI_ARGMAX, argmax_out=k2, seen=seen, vocab=V, penalty=1.2)
+    # the prologue's LN rounds to bf16 like the reference up to last-bit ties, so compare the
+    # winning columns per 64-column group (nearly all equal) and the per-row argmax
+    cols1, cols2 = (~k1) & 0xFFFFFFFF, (~k2) & 0xFFFFFFFF
+    assert (cols1 == cols2).float().mean().item() > 0.97
+    assert torch.equal((~ops.argmax_reduce(k1)) & 0xFFFFFFFF, (~ops.argmax_reduce(k2)) & 0xFFFFFFFF)
+
+
 def _attn_ref(q, kc, vc, slot, kvlen):
     R = q.shape[0]
     H = kc.shape[1]
