@@ -20,6 +20,7 @@
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
 #   e2e:<n>          scripts/run_config.py --config n (Raft cluster + gate + tutor) -> gpurun_out/e2e_<n>.log
+#   e2e1:<n>         the same with the tutor at TP=1 (one-GPU boxes: configs 4/5 ask for TP=4/8)
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
 #   sweep1:<...>     the same at batch 1 and 2 (p50 per query)     -> gpurun_out/sweep1.jsonl
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -89,6 +90,8 @@ for task in "$@"; do
                      --modes continuous; grep '^{' gpurun_out/serving.jsonl ;;
         e2e:*) step 900 gpurun_out/e2e_${task#e2e:}.log python -u scripts/run_config.py --config ${task#e2e:}
                tail -3 gpurun_out/e2e_${task#e2e:}.log ;;
+        e2e1:*) step 900 gpurun_out/e2e_${task#e2e1:}_tp1.log python -u scripts/run_config.py --config ${task#e2e1:} --tp 1
+                tail -3 gpurun_out/e2e_${task#e2e1:}_tp1.log ;;
         sweep:*)
             IFS=';' read -ra sets <<< "${task#sweep:}"
             for envs in "${sets[@]}"; do
