@@ -97,6 +97,7 @@ class _Rows:
     split_cap: int = 8  # split-K cap of the row-parallel projections (lower for concurrent row parts)
     split_fixed: int | None = None  # pinned split-K (M-independent arithmetic: prefill_split)
     persist_attn: bool = False  # decode attention as the low-occupancy persistent kernel
+    part: bool = False  # one of several concurrent row parts (no shared-workspace kernels)
 
 
 class HostResult:
@@ -220,6 +221,9 @@ class HipGPT2Engine:
         # (batch 1: 37.3 vs 35.9 ms per query, profiles/r2_lm_head_b1.txt)
         self.lm_ln_fused = os.environ.get("DLMS_LM_LN_FUSED", "0") == "1"
         self.alt_attn = os.environ.get("DLMS_OVERLAP_ALT_ATTN", "0") == "1"
+        # 16-32 rows: this many latency-path parts on as many HIP streams (0/1 = off)
+        self.small_overlap_parts = int(os.environ.get("DLMS_SMALL_OVERLAP_PARTS", "0"))  # measured slower (docs/PERFORMANCE.md)
+        self._in_small_overlap = False
         self.prefill_graphs = os.environ.get("DLMS_PREFILL_GRAPH", "1") != "0"
         self._pgraphs: dict[tuple[int, int], dict] = {}
         self._pseen: dict[tuple[int, int], int] = {}
@@ -626,21 +630,26 @@ class HipGPT2Engine:
     def _small_ok(self, B: int) -> bool:
         return 0 < B <= self.small_max
 
-    def _decode_step_small(self, B: int, penalty: float):
+    def _decode_step_small(self, B: int, penalty: float, lo: int = 0):
         """Latency-shaped decode step for B <= ``small_max`` rows: per layer
         [add+LN1+QKV] -> split-K attention -> out-proj (split-K partials) -> [add+LN2+c_fc+GELU]
         -> c_proj (partials); the residual ping-pongs between ``x`` and ``x2`` (every workgroup of a
         fused add+LN kernel re-reads its input rows, so the updated rows go to the other buffer).
-        Under TP the partial is all-reduced first and summed as one slab."""
+        Under TP the partial is all-reduced first and summed as one slab.  ``lo``: run on rows
+        [lo, lo + B) only (one part of the multi-stream small step, TP=1)."""
         eps = self.cfg.layer_norm_epsilon
-        r = self._rows(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
-                       self.cur_kvlen[:B], B)
-        bufs = (self.x[:B], self.x2[:B])
+        hi = lo + B
+        r = self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
+                       self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], B)
+        r.part = self._in_small_overlap
+        bufs = (self.x[lo:hi], self.x2[lo:hi])
         cur = 0
         pend = None  # (nsplit, residual bias) still to be added into x
         tp = self.tp_size > 1
         split = 1 if tp else self.SMALL_SPLIT
-        parts = self.parts[:, :B]
+        parts = self.parts[:, lo:hi]
+        if lo and (tp or not self.small_inplace):
+            raise ValueError("row-offset small step is TP=1 / in-place only")
         # TP=1: the row-parallel projections add straight into the residual (skinny MFMA, column-
         # owning, x += a W^T + b in place: no split-K slabs for the next kernel to sum)
         inplace = not tp and self.small_inplace
@@ -661,17 +670,17 @@ class HipGPT2Engine:
                                       parts=parts, nsplit=pend[0], res_bias=pend[1], bias=lw.b_qkv, q_out=r.q,
                                       k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
                 cur = 1 - cur
-            if self.fuse_ao and B == 1 and self.ao_groups:
+            if self.fuse_ao and B == 1 and self.ao_groups and not r.part:
                 # heads in groups of H/4: exactly the 4 slabs the fused add+LN sums cheaply
                 ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
                                             self.ao_groups, tiles=self.ao_group_tiles)
                 mlp_parts, ns, rb = self.ao_parts[:4, :1], 4, lw.b_o
-            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
+            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS and not r.part:
                 ops.attention_oproj(self.q[:B], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts)
                 mlp_parts, ns, rb = self.ao_parts[:, :B], self.w.n_heads_local, lw.b_o
             elif inplace:
                 self._attn(r, li)
-                ops.skinny_gemm(self.att[:B], lw.w_o_sh, ops.EPI_F32, bias=lw.b_o, out=bufs[cur])
+                ops.skinny_gemm(self.att[lo:hi], lw.w_o_sh, ops.EPI_F32, bias=lw.b_o, out=bufs[cur])
                 mlp_parts, ns, rb = None, 0, None
             else:
                 self._attn(r, li)
@@ -685,11 +694,11 @@ class HipGPT2Engine:
                 ops.skinny_addln_gemm(bufs[cur], lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps,
                                       bias=lw.b_fc, out=r.ff)
             if inplace:
-                ops.skinny_gemm(self.ff[:B], lw.w_p_sh, ops.EPI_F32, bias=lw.b_p, out=bufs[cur])
+                ops.skinny_gemm(self.ff[lo:hi], lw.w_p_sh, ops.EPI_F32, bias=lw.b_p, out=bufs[cur])
                 pend = None
             else:
                 pend = (row_parallel(r.ff, lw.w_p), lw.b_p)
-        if pend is None and self.lm_ln_fused:
+        if pend is None and self.lm_ln_fused and not lo:
             # ln_f in the LM head's prologue: every workgroup normalises the (few) rows itself
             ops.skinny_gemm(bufs[cur], self.lm_head_sh, ops.EPI_ARGMAX, ln=(self.w.lnf_g, self.w.lnf_b, eps),
                             argmax_out=self.key_parts[:B], seen=self.seen[:B], vocab=self.cfg.vocab_size,
@@ -697,15 +706,44 @@ class HipGPT2Engine:
             self._lm_head_and_update(None, B, penalty, keys_ready=True)
             return
         if pend is None:
-            ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, out_bf16=self.h[:B])
+            ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, out_bf16=self.h[lo:hi])
         else:
             ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, parts=self.parts, nsplit=pend[0],
                               bias=pend[1], out_bf16=self.h[:B])
-        self._lm_head_and_update(self.h[:B], B, penalty)
+        self._lm_head_and_update(self.h[lo:hi], B, penalty, lo=lo)
+
+    def _small_overlap_ok(self, B: int) -> bool:
+        k = self.small_overlap_parts
+        return (k > 1 and self.small_inplace and B > self.small_max and B % k == 0 and
+                B // k <= self.small_max and B <= self.x2.shape[0])
+
+    def _decode_step_small_overlap(self, B: int, penalty: float):
+        """16-32 rows as ``small_overlap_parts`` latency-path parts of <= small_max rows on as many
+        HIP streams: every kernel of the small step fills only a fraction of the CUs (36-192
+        workgroups), so independent row ranges run side by side instead of one tiled chain."""
+        k = self.small_overlap_parts
+        cur = torch.cuda.current_stream(self.device)
+        while len(self._side_streams) < k - 1:
+            self._side_streams.append(torch.cuda.Stream(device=self.device))
+        streams = [cur] + self._side_streams[: k - 1]
+        for s in streams[1:]:
+            s.wait_stream(cur)
+        step = B // k
+        self._in_small_overlap = True
+        try:
+            for i, s in enumerate(streams):
+                with torch.cuda.stream(s):
+                    self._decode_step_small(step, penalty, lo=i * step)
+        finally:
+            self._in_small_overlap = False
+        for s in streams[1:]:
+            cur.wait_stream(s)
 
     def _decode_step(self, B: int, penalty: float):
         if self._small_ok(B):
             return self._decode_step_small(B, penalty)
+        if self._small_overlap_ok(B):
+            return self._decode_step_small_overlap(B, penalty)
         if self._overlap_ok(B):
             return self._decode_step_overlap(B, penalty)
         self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
@@ -727,6 +765,8 @@ class HipGPT2Engine:
                 self._decode_step(B, penalty)
             torch.cuda.current_stream().wait_stream(s)
             self._restore_state(B, saved)
+            # (one graph per row part replayed on its own stream measured identical to this one
+            # forked graph: 668.07 vs 668.08 k tok/s, profiles/r2_sweep_split_graphs.jsonl)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._decode_step(B, penalty)

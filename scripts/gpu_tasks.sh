@@ -23,6 +23,7 @@
 #   e2e1:<n>         the same with the tutor at TP=1 (one-GPU boxes: configs 4/5 ask for TP=4/8)
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
 #   sweep1:<...>     the same at batch 1 and 2 (p50 per query)     -> gpurun_out/sweep1.jsonl
+#   sweep32:<...>    the same at batch 16 and 32                   -> gpurun_out/sweep1.jsonl
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 180 --timeout-method thread"
@@ -57,8 +58,11 @@ for task in "$@"; do
         test:*) step 600 gpurun_out/test_sel.log $T -m gpu ${task#test:}; tail -2 gpurun_out/test_sel.log ;;
         smoke) step 300 gpurun_out/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; tail -2 gpurun_out/smoke.log ;;
         bench) step 600 gpurun_out/bench.log python -u bench.py; grep '^{' gpurun_out/bench.log | tail -1 ;;
+        benchng) step 600 gpurun_out/bench_ng.log python -u bench.py --no-graph --latency-batches 32
+                 grep '^{' gpurun_out/bench_ng.log | tail -1 ;;
         prof:*) prof "${task#prof:}" --steps 5 --warmup 2 --latency-batches "" ;;
         prof1:*) prof "${task#prof1:}" --batch 1 --steps 3 --warmup 1 --latency-batches "" ;;
+        prof32:*) prof "${task#prof32:}" --batch 32 --steps 3 --warmup 1 --latency-batches "" ;;
         pmc:*)
             spec=${task#pmc:}; tag=${spec%%:*}; batch=${spec#*:}; export TMPDIR=/tmp; D=gpurun_out/pmc_$tag; mkdir -p $D
             passes=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
@@ -99,10 +103,11 @@ for task in "$@"; do
                 echo "{\"env\": \"$envs\", \"bench\": $(grep '^{' gpurun_out/sweep.log | tail -1)}" >> gpurun_out/sweep.jsonl
                 tail -1 gpurun_out/sweep.jsonl
             done ;;
-        sweep1:*)  # the same at batch 1 and 2 (latency path): value = tok/s, plus p50 per query
-            IFS=';' read -ra sets <<< "${task#sweep1:}"
+        sweep1:*|sweep32:*)  # the same at batch 1 and 2 / 16 and 32: value = tok/s, plus p50 per query
+            IFS=';' read -ra sets <<< "${task#*:}"
+            bs="1 2"; [[ $task == sweep32:* ]] && bs="16 32"
             for envs in "${sets[@]}"; do
-                for b in 1 2; do
+                for b in $bs; do
                     step 300 gpurun_out/sweep1.log env ${envs//,/ } python -u bench.py --batch $b --steps 8 --warmup 2 --latency-batches ""
                     echo "{\"env\": \"$envs\", \"batch\": $b, \"bench\": $(grep '^{' gpurun_out/sweep1.log | tail -1)}" >> gpurun_out/sweep1.jsonl
                 done

@@ -104,6 +104,31 @@ def test_graph_replay_equals_eager():
     assert a == b
 
 
+@pytest.mark.parametrize("batch,parts", [(16, 4), (32, 4), (16, 2)])
+def test_small_overlap_equals_tiled(batch, parts, monkeypatch):
+    """16-32 rows as latency-path parts on several streams: the same tokens as the single-stream
+    tiled path wherever the fp32 oracle is decisive, and identical across graph / eager."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+    from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, teacher_forced_check
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [5 + (3 * i) % 29 for i in range(batch)], seed=7)
+    monkeypatch.setenv("DLMS_SMALL_OVERLAP_PARTS", str(parts))
+    ov = HipGPT2Engine(cfg, w, max_batch=batch, max_length=48)
+    assert ov._small_overlap_ok(batch)
+    a = ov.generate(prompts)
+    ov_eager = HipGPT2Engine(cfg, w, max_batch=batch, max_length=48, use_graph=False)
+    assert ov_eager.generate(prompts) == a
+    oracle = GPT2Reference(cfg, w, device="cuda")
+    decisive = total = 0
+    for o, p in zip(a, prompts):
+        res = teacher_forced_check(oracle, o, len(p), 1.2, eps=0.05)
+        assert not res["mismatches"], res["mismatches"]
+        decisive += res["decisive"]
+        total += res["positions"]
+    assert decisive >= 0.7 * total
+
+
 def test_prefill_graph_equals_eager():
     """A (rows, prompts) prefill shape seen twice is replayed from a hipGraph (padded tile table):
     tokens bit-identical to eager prefills, also for a different length mix of the same shape and
