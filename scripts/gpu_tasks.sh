@@ -88,6 +88,7 @@ for task in "$@"; do
                    step 300 gpurun_out/skinny_cold.jsonl python -u scripts/bench_skinny.py --batches 1 --cold-mb 512 --T 150 ;;
         attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
         pgemm) step 300 gpurun_out/pgemm.jsonl python -u scripts/bench_prefill_gemm.py; grep '^{' gpurun_out/pgemm.jsonl ;;
+        conc) step 300 gpurun_out/conc.jsonl python -u scripts/bench_concurrency.py; grep '^{' gpurun_out/conc.jsonl ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
         gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;
         serving) step 400 gpurun_out/serving.jsonl python -u scripts/bench_serving.py --rates 20,200,1000 --queries 400 \
