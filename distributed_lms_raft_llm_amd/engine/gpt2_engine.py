@@ -884,6 +884,8 @@ class HipGPT2Engine:
         key = (R, n)
         if key in self._pgraphs:
             return True
+        if len(self._pseen) > 8192:  # shapes seen once: a bounded memory of candidates
+            self._pseen.clear()
         self._pseen[key] = self._pseen.get(key, 0) + 1
         return self._pseen[key] >= 2 and len(self._pgraphs) < self.PREFILL_GRAPH_CACHE
 

@@ -91,6 +91,8 @@ for task in "$@"; do
         conc) step 300 gpurun_out/conc.jsonl python -u scripts/bench_concurrency.py; grep '^{' gpurun_out/conc.jsonl ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
         gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;
+        serving5) step 300 gpurun_out/serving5.jsonl python -u scripts/bench_serving.py --rates 5 --queries 100 \
+                      --modes continuous --prompt-jitter 0; grep '^{' gpurun_out/serving5.jsonl ;;
         serving) step 400 gpurun_out/serving.jsonl python -u scripts/bench_serving.py --rates 20,200,1000 --queries 400 \
                      --modes continuous; grep '^{' gpurun_out/serving.jsonl ;;
         e2e:*) step 900 gpurun_out/e2e_${task#e2e:}.log python -u scripts/run_config.py --config ${task#e2e:}

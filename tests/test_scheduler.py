@@ -106,6 +106,30 @@ def test_outputs_match_solo_runs_with_staggered_arrivals():
     assert max(eng.buckets) <= 4
 
 
+def test_decode_chunks_capped_by_remaining_budget():
+    """A lone request decodes at most one step past its max_length budget (no whole no-op chunk
+    at the end of every query): prompt 7, max_length 40 -> 32 decode steps needed."""
+    eng = FakeSlotEngine(max_batch=4, max_length=40)
+    eng.stop_at_eos = False  # every sequence runs to max_length
+    steps = []
+    orig = eng.decode
+
+    def decode(B, n, penalty):
+        steps.append(n)
+        orig(B, n, penalty)
+
+    eng.decode = decode
+    cb = ContinuousBatcher(eng, chunk=8)
+    try:
+        out = cb.submit([1, 2, 3, 4, 5, 6, 7]).result(10)
+    finally:
+        cb.stop()
+    assert len(out) == 40
+    need = 40 - 7 - 1
+    assert need <= sum(steps) <= need + 1, steps
+    assert steps[:4] == [8, 8, 8, 8]
+
+
 def test_passthrough_and_empty_prompt():
     eng = FakeSlotEngine(max_batch=2, max_length=10)
     cb = ContinuousBatcher(eng)
