@@ -616,7 +616,10 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
 
     float m = -INFINITY, l = 0.f;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    constexpr int U = 4;
+#ifndef DLMS_SPLIT_U
+#define DLMS_SPLIT_U 4
+#endif
+    constexpr int U = DLMS_SPLIT_U;  // key groups of 8 in flight per wave
     for (int t0 = t_lo; t0 < t_hi; t0 += 8 * U) {
         uint4 kr[U], vr[U];
 #pragma unroll
