@@ -1,6 +1,7 @@
 // LayerNorm family (K2, K13).  One wave per row, the whole row held in registers
 // (float4 loads, up to 8 per lane => d <= 2048), two-pass statistics in fp32.
 #include "common.h"
+#include <stdlib.h>
 
 #define LN_MAX_V4 8  // float4 per lane -> d <= 64*4*8 = 2048
 
@@ -129,7 +130,7 @@ extern "C" hipError_t dlms_layernorm_gather(const float* x, int ldx, const int* 
 // This consumes the split-K partial slabs of the previous projection GEMM (EPI_PARTIAL) or, under
 // tensor parallelism, the all-reduced partial, so no GEMM epilogue ever read-modify-writes x.
 template <int NSPLIT, int NV4>
-__global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x, int ldx,
+__global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ x, int ldx,
                                                            const float* __restrict__ parts, int ldp,
                                                            long long split_stride, const float* __restrict__ bias,
                                                            const float* __restrict__ gamma,
@@ -137,8 +138,8 @@ __global__ __launch_bounds__(64) void add_layernorm_kernel(float* __restrict__ x
                                                            int ldb, unsigned int* __restrict__ out8, int ld8,
                                                            float* __restrict__ out8_scale, int M, int D, float eps,
                                                            int store_normed) {
-    const int lane = threadIdx.x;
-    const int row = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);  // one wave per row
     if (row >= M) return;
     const int nv = D >> 2;
     float4* xr = reinterpret_cast<float4*>(x + (size_t)row * ldx);
@@ -278,15 +279,25 @@ extern "C" hipError_t dlms_quantize_rows_fp8(const void* a, int lda, void* q, in
     return hipGetLastError();
 }
 
+// rows (waves) per workgroup of add_layernorm_kernel: DLMS_LN_ROWS_PER_BLOCK (1 or 4)
+static int ln_rows_per_block() {
+    static int v = 0;
+    if (v == 0) {
+        const char* e = getenv("DLMS_LN_ROWS_PER_BLOCK");
+        v = (e != nullptr && e[0] == '4') ? 4 : 1;
+    }
+    return v;
+}
+
 template <int NSPLIT>
-static void launch_add_ln(int nv4, dim3 grid, hipStream_t stream, float* x, int ldx, const float* parts, int ldp,
+static void launch_add_ln(int nv4, dim3 grid, int rpb, hipStream_t stream, float* x, int ldx, const float* parts, int ldp,
                           long long split_stride, const float* bias, const float* gamma, const float* beta,
                           bf16_t* o, int ldb, unsigned int* o8, int ld8, float* o8s, int M, int D, float eps,
                           int store_normed) {
 #define ADD_LN_V(V)                                                                                            \
     case V:                                                                                                    \
-        hipLaunchKernelGGL((add_layernorm_kernel<NSPLIT, V>), grid, dim3(64), 0, stream, x, ldx, parts, ldp,    \
-                           split_stride, bias, gamma, beta, o, ldb, o8, ld8, o8s, M, D, eps, store_normed);    \
+        hipLaunchKernelGGL((add_layernorm_kernel<NSPLIT, V>), grid, dim3(64 * rpb), 0, stream, x, ldx, parts,  \
+                           ldp, split_stride, bias, gamma, beta, o, ldb, o8, ld8, o8s, M, D, eps, store_normed); \
         break;
     switch (nv4) {
         ADD_LN_V(1) ADD_LN_V(2) ADD_LN_V(3) ADD_LN_V(4) ADD_LN_V(5) ADD_LN_V(6) ADD_LN_V(7) ADD_LN_V(8)
@@ -301,9 +312,11 @@ extern "C" hipError_t dlms_add_layernorm(float* x, int ldx, const float* parts, 
     if (D % 4 != 0 || D > 64 * 4 * LN_MAX_V4 || M <= 0 || nsplit < 0 || nsplit > 8) return hipErrorInvalidValue;
     bf16_t* o = reinterpret_cast<bf16_t*>(out_bf16);
     const int nv4 = (D / 4 + 63) / 64;
+    const int rpb = ln_rows_per_block();
 #define ADD_LN_CASE(NS)                                                                                       \
     case NS:                                                                                                  \
-        launch_add_ln<NS>(nv4, dim3(M), stream, x, ldx, parts, ldp, split_stride, bias, gamma, beta, o, ldb,       \
+        launch_add_ln<NS>(nv4, dim3((M + rpb - 1) / rpb), rpb, stream, x, ldx, parts, ldp, split_stride, bias, \
+                          gamma, beta, o, ldb,                                                                \
                           reinterpret_cast<unsigned int*>(out_fp8), ld8, out_fp8_scale, M, D, eps, store_normed); \
         break;
     switch (nsplit) {

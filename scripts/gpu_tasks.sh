@@ -56,6 +56,9 @@ for task in "$@"; do
     case "$task" in
         tests) step 900 gpurun_out/tests.log $T -m gpu tests/; tail -2 gpurun_out/tests.log ;;
         test:*) step 600 gpurun_out/test_sel.log $T -m gpu ${task#test:}; tail -2 gpurun_out/test_sel.log ;;
+        testenv:*)  # testenv:<ENV=v>:<paths>  one gpu test selection under an environment setting
+            spec=${task#testenv:}; envs=${spec%%:*}; paths=${spec#*:}
+            step 600 gpurun_out/test_env.log env ${envs//,/ } $T -m gpu $paths; tail -2 gpurun_out/test_env.log ;;
         smoke) step 300 gpurun_out/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; tail -2 gpurun_out/smoke.log ;;
         bench) step 600 gpurun_out/bench.log python -u bench.py; grep '^{' gpurun_out/bench.log | tail -1 ;;
         benchng) step 600 gpurun_out/bench_ng.log python -u bench.py --no-graph --latency-batches 32
