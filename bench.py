@@ -206,6 +206,8 @@ def main():
             "p50_query_latency_ms": round(p50, 3),
             "baseline_p50_query_latency_ms": 2198,
             "new_tokens_per_step": total_new / args.steps,
+            "prefill_ms": round(stats.prefill_ms / max(1, args.steps), 3),  # per generation, this rank
+            "decode_ms": round(stats.decode_ms / max(1, args.steps), 3),
             **extra,
             "config": {
                 "model": f"{args.model} ({cfg.num_params() / 1e6:.0f}M)",
