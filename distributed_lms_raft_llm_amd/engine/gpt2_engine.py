@@ -273,6 +273,15 @@ class HipGPT2Engine:
         self.ao_group_tiles = int(os.environ.get("DLMS_AO_GROUP_TILES", "3"))
         if self.ao_groups and (cfg.n_embd // 16) % self.ao_group_tiles:
             self.ao_group_tiles = 1
+        # batch 1 (TP=1, head-grouped attention): LN2 -> c_fc -> GELU -> c_proj as ONE kernel whose
+        # workgroups add their 16-column slices into an int64 fixed-point residual (order-independent
+        # integer atomics; ops.skinny_mlp) -- one launch and one dependent round trip fewer per layer
+        self.fused_mlp = (self.ao_groups > 0 and cfg.n_embd in (768, 1024) and self.w.ffn_local == 4 * cfg.n_embd and
+                          os.environ.get("DLMS_FUSED_MLP", "1") != "0")
+        if self.fused_mlp:
+            for lw in self.w.layers:
+                if lw.w_p_sl is None:
+                    lw.w_p_sl = ops.slice_cproj(lw.w_p)
         # LM head of the throughput path (>= PS_LM_MIN_ROWS rows): panel-resident gemm_ps on a
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
@@ -308,6 +317,8 @@ class HipGPT2Engine:
         self.x = torch.zeros(B, D, dtype=f32, device=dev)
         # second residual buffer: the latency path's fused add+LN kernels advance x by ping-pong
         self.x2 = torch.zeros(min(B, 64), D, dtype=f32, device=dev)
+        # the fused MLP's ping-pong int64 fixed-point residual (batch 1)
+        self.xr = torch.zeros(2, ops.fix_copies(), 1, D, dtype=torch.int64, device=dev) if self.fused_mlp else None
         # cross-workgroup split attention (few rows, long caches): partials + arrival counters
         self.attn_ws = ops.AttnSplitWorkspace(self.SPLIT_ATTN_MAX_PAIRS, 2, dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
@@ -660,6 +671,11 @@ class HipGPT2Engine:
                 self._all_reduce(self.parts[0, :B])
             return split
 
+        if inplace and self.fused_mlp and B == 1 and not r.part and not lo:
+            self._decode_layers_fused_mlp(r, B)
+            ops.ln_fix(self.xr[(len(self.w.layers) - 1) % 2, :, :B], self.w.lnf_g, self.w.lnf_b, eps, self.h[:B])
+            self._lm_head_and_update(self.h[:B], B, penalty)
+            return
         for li, lw in enumerate(self.w.layers):
             kc, vc = self.kv[li, 0], self.kv[li, 1]
             if pend is None:
@@ -711,6 +727,24 @@ class HipGPT2Engine:
             ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, parts=self.parts, nsplit=pend[0],
                               bias=pend[1], out_bf16=self.h[:B])
         self._lm_head_and_update(self.h[lo:hi], B, penalty, lo=lo)
+
+    def _decode_layers_fused_mlp(self, r, B: int):
+        """Batch-1 layers as three kernels each: [LN1 + QKV (+ clear the MLP's accumulator)] ->
+        [attention + out-projection, 4 head-group slabs] -> [add + LN2 + c_fc + GELU + c_proj, added
+        into the int64 fixed-point residual xr[l % 2]].  Layer 0 reads the f32 embedding row x; the
+        final residual is xr[(L - 1) % 2]."""
+        eps = self.cfg.layer_norm_epsilon
+        xin = self.x[:B]
+        for li, lw in enumerate(self.w.layers):
+            kc, vc = self.kv[li, 0], self.kv[li, 1]
+            acc = self.xr[li % 2, :, :B]
+            ops.skinny_addln_gemm(xin, lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, bias=lw.b_qkv, q_out=r.q,
+                                  k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos, zero=acc)
+            ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
+                                        self.ao_groups, tiles=self.ao_group_tiles)
+            ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc,
+                           parts=self.ao_parts[:4, :1], nsplit=4, res_bias=lw.b_o)
+            xin = acc
 
     def _small_overlap_ok(self, B: int) -> bool:
         k = self.small_overlap_parts

@@ -60,6 +60,7 @@ class LayerWeights:
     w_fc_sh: torch.Tensor | None = None
     w_o_sh: torch.Tensor | None = None  # fused attention + out-projection / in-place out-proj
     w_p_sh: torch.Tensor | None = None  # in-place c_proj (latency path, TP=1)
+    w_p_sl: torch.Tensor | None = None  # fused batch-1 MLP: c_proj in 16-column slabs (ops.slice_cproj)
 
 
 @dataclass

@@ -58,17 +58,19 @@ def needs_build(checked: bool = False) -> bool:
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False, checked: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, checked: bool = False, out: str | None = None,
+          defines: tuple[str, ...] = ()) -> Path:
     """Compile every kernel source for gfx950 into the in-tree shared library (``checked``: the
-    debug variant with device-side index range checks, ``-DDLMS_DEVICE_CHECKS=1``)."""
-    path = CHECKED_LIB_PATH if checked else LIB_PATH
-    if not force and not needs_build(checked):
+    debug variant with device-side index range checks, ``-DDLMS_DEVICE_CHECKS=1``).  ``out`` +
+    ``defines`` (``NAME=VALUE``): an A/B variant for experiments (loaded via ``DLMS_HIP_LIB``)."""
+    path = Path(out) if out else (CHECKED_LIB_PATH if checked else LIB_PATH)
+    if not out and not force and not needs_build(checked):
         return path
-    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    path.parent.mkdir(parents=True, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = path.with_suffix(f".so.tmp{os.getpid()}")
     flags = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wno-unused-result"] + \
-        (["-DDLMS_DEVICE_CHECKS=1"] if checked else [])
+        (["-DDLMS_DEVICE_CHECKS=1"] if checked else []) + [f"-D{d}" for d in defines]
     # one hipcc per translation unit, in parallel (the kernels of a unit never call another
     # unit's device code, so no relocatable device code is needed), then one link
     import tempfile
@@ -152,7 +154,11 @@ def _bind(L):
         "dlms_attention_oproj": [P, I, P, P, P, P, I, I, I, I, F, P, I, I, P, I, ctypes.c_longlong, P],
         "dlms_attention_oproj_grouped": [P, P, P, P, P, I, I, I, I, F, P, I, I, P, ctypes.c_longlong, P],
         "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
-                                   ctypes.POINTER(GemmEpi), P],
+                                   ctypes.POINTER(GemmEpi), I, ctypes.c_longlong, P, I, P],
+        "dlms_skinny_mlp": [P, I, I, ctypes.c_longlong, P, I, ctypes.c_longlong, I, P, P, P, F, P, P, P, P, P, I,
+                            ctypes.c_longlong, I, I, I, P],
+        "dlms_ln_fix": [P, I, ctypes.c_longlong, P, P, F, P, I, I, I, P],
+        "dlms_fix_copies": [],
         "dlms_skinny_addln_max_rows": [I],
         "dlms_gemm_ps": [I, P, I, P, I, I, I, I, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_attention_persist": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, P],
@@ -803,7 +809,7 @@ def skinny_addln_max_rows(K: int) -> int:
 
 def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, beta, eps: float, *, x_out=None,
                       parts=None, nsplit: int = 0, res_bias=None, bias=None, out=None, q_out=None, k_cache=None,
-                      v_cache=None, row_slot=None, row_pos=None):
+                      v_cache=None, row_slot=None, row_pos=None, zero=None):
     """Fused residual update + LayerNorm + skinny GEMM (decode LN1 -> QKV, LN2 -> c_fc) for
     M <= ``skinny_addln_max_rows(K)`` rows:
 
@@ -812,8 +818,30 @@ def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, b
 
     ``x_out`` must not alias ``x_in`` (every workgroup re-reads x_in; one of them writes x_out):
     the engine ping-pongs two residual buffers.  nsplit in {0, 1, 4}, or 12 / 16 (per-head slabs of
-    ``attention_oproj``; M <= 4, K <= 1024)."""
-    _req(x_in, torch.float32, "x_in", 2)
+    ``attention_oproj``; M <= 4, K <= 1024).
+
+    ``x_in`` may be the int64 fixed-point residual a ``skinny_mlp`` left ([FIX_COPIES, M, K]; QKV
+    epilogue, no slabs, no x_out); ``zero``: a contiguous tensor (the next ``skinny_mlp``'s
+    accumulator) the kernel clears on the side."""
+    xfix = x_in.dtype == torch.int64
+    xcs = 0
+    if xfix:
+        if epi != EPI_QKV or nsplit or x_out is not None:
+            raise ValueError("skinny_addln_gemm: a fixed-point residual feeds only the QKV epilogue, no slabs")
+        _req(x_in, torch.int64, "x_in", 3)
+        if x_in.shape[0] != fix_copies() or x_in.stride(0) % 2:
+            raise ValueError(f"skinny_addln_gemm: fixed-point x_in must be [{fix_copies()}, M, K]")
+        xcs = x_in.stride(0)
+        x_in = x_in[0]
+    else:
+        _req(x_in, torch.float32, "x_in", 2)
+    zchunks = 0
+    if zero is not None:
+        if not zero.is_contiguous() or zero.data_ptr() % 16 or (zero.numel() * zero.element_size()) % 16:
+            raise ValueError("skinny_addln_gemm: zero must be a contiguous 16-byte multiple")
+        if zero.data_ptr() == x_in.data_ptr():
+            raise ValueError("skinny_addln_gemm: zero must not alias x_in")
+        zchunks = zero.numel() * zero.element_size() // 16
     _req(w_sh, torch.bfloat16, "w_sh", 4)
     G, KB = w_sh.shape[0], w_sh.shape[1]
     if w_sh.shape[2] != 64 or w_sh.shape[3] != 8 or not w_sh.is_contiguous():
@@ -847,7 +875,7 @@ def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, b
             raise ValueError("skinny_addln_gemm: x_out must match x_in's layout")
         if x_out.data_ptr() == x_in.data_ptr():
             raise ValueError("skinny_addln_gemm: x_out must not alias x_in (ping-pong the residual)")
-    if x_in.stride(0) % 4 or x_in.data_ptr() % 16:
+    if x_in.stride(0) % 4 or x_in.data_ptr() % 16 or not x_in.stride(1) == 1:
         raise ValueError("skinny_addln_gemm: x rows must be 16-byte aligned")
     ep = GemmEpi()
     if bias is not None:
@@ -884,7 +912,115 @@ def skinny_addln_gemm(x_in: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, b
         raise ValueError("skinny_addln_gemm: QKV or GELU epilogue")
     _check(lib().dlms_skinny_addln_gemm(epi, _p(x_in), _p(x_out), x_in.stride(0), _p(parts) if nsplit else None, ldp,
                                         sstride, nsplit, _p(res_bias), _p(gamma), _p(beta), float(eps), _p(w_sh), M, N,
-                                        K, ctypes.byref(ep), _stream()), "dlms_skinny_addln_gemm")
+                                        K, ctypes.byref(ep), int(xfix), xcs, _p(zero), zchunks, _stream()),
+           "dlms_skinny_addln_gemm")
+    return out
+
+
+def slice_cproj(w_p: torch.Tensor) -> torch.Tensor:
+    """c_proj weight [d, F] (F = 4d contiguous) -> [F/16, d, 16]: the contiguous 16-column slab each
+    ``skinny_mlp`` workgroup streams."""
+    if w_p.dim() != 2 or w_p.shape[1] % 16:
+        raise ValueError(f"slice_cproj: need [d, F % 16], got {tuple(w_p.shape)}")
+    d, F = w_p.shape
+    return w_p.reshape(d, F // 16, 16).permute(1, 0, 2).contiguous()
+
+
+FIX_SCALE = float(2 ** 32)  # skinny.hip DLMS_FIX_SCALE: the fused MLP's int64 fixed-point residual
+
+
+def fix_copies() -> int:
+    """Partial copies of the fixed-point residual ([fix_copies(), M, d]; readers sum them)."""
+    return int(lib().dlms_fix_copies())
+
+
+def fix_to_float(r: torch.Tensor) -> torch.Tensor:
+    """int64 fixed-point residual [fix_copies(), M, d] -> f32 [M, d] (tests / debugging)."""
+    return (r.sum(0).to(torch.float64) / FIX_SCALE).to(torch.float32)
+
+
+def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tensor, b_fc, w_p_sl: torch.Tensor, b_p,
+               r_out: torch.Tensor, *, parts=None, nsplit: int = 0, res_bias=None):
+    """Fused latency-path MLP (TP=1, M <= 8 rows, d in {768, 1024}):
+
+        v = x_in + res_bias + sum(parts[:nsplit]);  h = bf16(gelu(bf16(LN(v)) @ W_fc.T + b_fc))
+        r_out += fix(v + h @ W_p.T + b_p)
+
+    ``x_in``: f32 [M, d] or int64 fixed point [fix_copies(), M, d]; ``r_out``: int64 fixed point
+    [fix_copies(), M, d], ZERO on entry (``skinny_addln_gemm(zero=...)`` clears it), must not alias
+    ``x_in``.  Workgroup j adds its contribution into copy j % fix_copies() with 64-bit integer
+    atomics: the result is order-independent."""
+    xfix = x_in.dtype == torch.int64
+    C = fix_copies()
+    xcs = 0
+    if xfix:
+        _req(x_in, torch.int64, "x_in", 3)
+        if x_in.shape[0] != C or x_in.stride(0) % 2:
+            raise ValueError(f"skinny_mlp: fixed-point x_in must be [{C}, M, d]")
+        xcs = x_in.stride(0)
+        x_in = x_in[0]
+    else:
+        _req(x_in, torch.float32, "x_in", 2)
+    _req(r_out, torch.int64, "r_out", 3)
+    if r_out.shape[0] != C or r_out.stride(0) % 2:
+        raise ValueError(f"skinny_mlp: r_out must be [{C}, M, d]")
+    rcs = r_out.stride(0)
+    r_full, r_out = r_out, r_out[0]
+    _req(w_fc_sh, torch.bfloat16, "w_fc_sh", 4)
+    _req(w_p_sl, torch.bfloat16, "w_p_sl", 3)
+    M, K = x_in.shape
+    F = w_fc_sh.shape[0] * 16
+    if w_fc_sh.shape[1] * 32 != K or not w_fc_sh.is_contiguous() or tuple(w_p_sl.shape) != (F // 16, K, 16) or \
+            not w_p_sl.is_contiguous():
+        raise ValueError("skinny_mlp: weight layouts (shuffle_weight / slice_cproj) do not match x_in")
+    if M < 1 or M > 8 or K not in (768, 1024):
+        raise ValueError(f"skinny_mlp: M <= 8 rows of width 768 / 1024, got {tuple(x_in.shape)}")
+    if r_out.shape[0] < M or r_out.shape[1] < K or r_out.stride(1) != 1 or r_out.data_ptr() == x_in.data_ptr():
+        raise ValueError("skinny_mlp: r_out too small or aliases x_in")
+    if x_in.stride(1) != 1 or x_in.stride(0) % 4 or x_in.data_ptr() % 16:
+        raise ValueError("skinny_mlp: x rows must be 16-byte aligned")
+    for t, n, size in ((gamma, "gamma", K), (beta, "beta", K), (b_fc, "b_fc", F), (b_p, "b_p", K)):
+        _req(t, torch.float32, n, 1)
+        if t.numel() != size:
+            raise ValueError(f"skinny_mlp: {n} size")
+    if nsplit not in (0, 4):
+        raise ValueError("skinny_mlp: nsplit in {0, 4}")
+    ldp, sstride = 0, 0
+    if nsplit:
+        _req(parts, torch.float32, "parts", 3)
+        if parts.shape[0] < nsplit or parts.shape[1] < M or parts.shape[2] < K or parts.stride(2) != 1 or \
+                parts.stride(1) % 4 or parts.stride(0) % 4:
+            raise ValueError("skinny_mlp: parts too small / misaligned")
+        ldp, sstride = parts.stride(1), parts.stride(0)
+    if res_bias is not None:
+        _req(res_bias, torch.float32, "res_bias", 1)
+        if res_bias.numel() != K:
+            raise ValueError("res_bias size")
+    _check(lib().dlms_skinny_mlp(_p(x_in), x_in.stride(0), int(xfix), xcs, _p(parts) if nsplit else None, ldp,
+                                 sstride, nsplit, _p(res_bias), _p(gamma), _p(beta), float(eps), _p(w_fc_sh), _p(b_fc),
+                                 _p(w_p_sl), _p(b_p), _p(r_out), r_out.stride(0), rcs, M, K, F, _stream()),
+           "dlms_skinny_mlp")
+    return r_full
+
+
+def ln_fix(x: torch.Tensor, gamma, beta, eps: float, out: torch.Tensor):
+    """LayerNorm of an int64 fixed-point residual [fix_copies(), M, K] -> bf16 ``out`` (ln_f after
+    ``skinny_mlp``)."""
+    _req(x, torch.int64, "x", 3)
+    _req(out, torch.bfloat16, "out", 2)
+    if x.shape[0] != fix_copies() or x.stride(0) % 2:
+        raise ValueError(f"ln_fix: x must be [{fix_copies()}, M, K]")
+    xcs, x = x.stride(0), x[0]
+    M, K = x.shape
+    if x.stride(1) != 1 or out.stride(1) != 1 or out.shape[0] < M or out.shape[1] < K or x.stride(0) % 2 or \
+            out.stride(0) % 4 or K % 4 or K > 2048 or x.data_ptr() % 16 or out.data_ptr() % 8:
+        raise ValueError("ln_fix: shapes / alignment")
+    for t, n in ((gamma, "gamma"), (beta, "beta")):
+        _req(t, torch.float32, n, 1)
+        if t.numel() != K:
+            raise ValueError(f"ln_fix: {n} size")
+    _check(lib().dlms_ln_fix(_p(x), x.stride(0), xcs, _p(gamma), _p(beta), float(eps), _p(out), out.stride(0), M, K,
+                             _stream()), "dlms_ln_fix")
     return out
 
 

@@ -361,6 +361,58 @@ extern "C" hipError_t dlms_skinny_gemm(int epi, const void* A, int lda, const fl
 #undef SK_NOLN
 }
 
+// The latency path's residual stream between fused MLP kernels is int64 fixed point (value * 2^32):
+// every workgroup of the MLP adds its slice's contribution with a 64-bit integer atomic, and integer
+// adds commute, so the sum is bit-identical whatever order the workgroups arrive in (float atomics
+// would not be).  |x| < 2^31 and a resolution of 2^-32 cover any GPT-2 residual with margin.
+// The residual is held as DLMS_FIX_COPIES partial copies (workgroup j adds into copy j % COPIES,
+// readers sum them): atomics to one address serialise at the memory side.  Batch-1 query in situ
+// (profiles/r2_fused_mlp.txt): 1 copy 36.9 ms, 2 copies 34.8, 4 copies 34.8 (8: the QKV prologue's
+// extra 6 KB per row and copy cost more than the contention saved).
+#ifndef DLMS_FIX_COPIES
+#define DLMS_FIX_COPIES 2
+#endif
+#define DLMS_FIX_SCALE 4294967296.0f
+#define DLMS_FIX_INV (1.0f / 4294967296.0f)
+
+__device__ __forceinline__ float fix_to_f32(long long v) { return (float)v * DLMS_FIX_INV; }
+__device__ __forceinline__ unsigned long long f32_to_fix(float v) {
+    return (unsigned long long)__float2ll_rn(v * DLMS_FIX_SCALE);
+}
+
+// 4 consecutive residual values (columns 4c..4c+3) of the row at element offset `off`: f32, or
+// int64 fixed point converted on load
+template <bool XFIX>
+__device__ __forceinline__ float4 load_resid4(const void* __restrict__ x, size_t off, int c, long long cs) {
+    if constexpr (XFIX) {  // sum of the copies (exact integer adds), then one rounding to f32
+        const long long* base = reinterpret_cast<const long long*>(x) + off + 4 * c;
+        longlong2 a[DLMS_FIX_COPIES], b[DLMS_FIX_COPIES];
+#pragma unroll
+        for (int k = 0; k < DLMS_FIX_COPIES; ++k) {
+            a[k] = reinterpret_cast<const longlong2*>(base + k * cs)[0];
+            b[k] = reinterpret_cast<const longlong2*>(base + k * cs)[1];
+        }
+#pragma unroll
+        for (int k = 1; k < DLMS_FIX_COPIES; ++k) {
+            a[0].x += a[k].x; a[0].y += a[k].y; b[0].x += b[k].x; b[0].y += b[k].y;
+        }
+        return make_float4(fix_to_f32(a[0].x), fix_to_f32(a[0].y), fix_to_f32(b[0].x), fix_to_f32(b[0].y));
+    } else {
+        return reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off)[c];
+    }
+}
+
+template <bool XFIX>
+__device__ __forceinline__ float load_resid1(const void* __restrict__ x, size_t off, long long cs) {
+    if constexpr (XFIX) {
+        long long a = 0;
+#pragma unroll
+        for (int k = 0; k < DLMS_FIX_COPIES; ++k) a += reinterpret_cast<const long long*>(x)[off + k * cs];
+        return fix_to_f32(a);
+    } else
+        return reinterpret_cast<const float*>(x)[off];
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fused residual update + LayerNorm + skinny GEMM: the decode path's LN1 -> QKV and LN2 -> c_fc at
 // M <= 4 * RPW rows (one 16-row MFMA tile; rows >= M are never stored).
@@ -373,33 +425,26 @@ extern "C" hipError_t dlms_skinny_gemm(int epi, const void* A, int lda, const fl
 //
 // Load order: all weight fragments of the wave first (HBM), then the activation rows (L2), so
 // both are in flight together -- one memory round trip before the LayerNorm, not two.
-template <int EPI, int NSPLIT, int NV4, int RPW, int KBW>
-__global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restrict__ x_in, float* __restrict__ x_out,
-                                                         int ldx, const float* __restrict__ parts, int ldp,
-                                                         long long split_stride, const float* __restrict__ res_bias,
-                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                         float eps, const bf16_t* __restrict__ Wsh, int M, int N, int K,
-                                                         GemmEpi ep) {
+// Fused-kernel prologue: rows [0, M) of v = x_in + res_bias + sum_{s < NSPLIT} parts[s] (wave w owns
+// rows w, w + 4, ...), written to x_out by block 0 when given, LayerNormed into the LDS bf16 image
+// (rows >= M are left as they are: their MFMA results are never stored).
+struct NoOp {
+    __device__ void operator()() const {}
+};
+
+// (after_loads() runs once the activation loads are issued: a caller's own loads issued there stay in
+// flight under the LayerNorm instead of delaying it)
+template <int NSPLIT, int NV4, int RPW, bool XFIX, typename AfterLoads = NoOp>
+__device__ __forceinline__ void addln_rows_lds(const void* __restrict__ x_in, float* __restrict__ x_out, int ldx,
+                                               const float* __restrict__ parts, int ldp, long long split_stride,
+                                               const float* __restrict__ res_bias, const float* __restrict__ gamma,
+                                               const float* __restrict__ beta, float eps, int M, int K, char* smem,
+                                               int row_bytes, long long xcs, float* v_lds = nullptr,
+                                               AfterLoads after_loads = AfterLoads()) {
     constexpr int NW = 4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int ng = blockIdx.x;
-    const int nkb = K >> 5;
-    const int per = (nkb + NW - 1) / NW;
-    const int kb0 = wave * per < nkb ? wave * per : nkb;
-    const int nk = (kb0 + per < nkb ? kb0 + per : nkb) - kb0;
-    const int kbl = nk > 0 ? kb0 : 0;
-    const int last = nk > 0 ? nk - 1 : 0;
-    const int g = lane >> 4, fr = lane & 15;
-    const int row_bytes = K * 2 + 16;
     const int nv = K >> 2;
-
-    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wsh) + ((size_t)ng * nkb + kbl) * 64 + lane;
-    bf16x8_t b[KBW];
-#pragma unroll
-    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
-
     int cidx[NV4];
     bool valid[NV4];
 #pragma unroll
@@ -414,9 +459,8 @@ __global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restri
     for (int i = 0; i < RPW; ++i) {
         int row = wave + NW * i;
         row = row < M ? row : M - 1;
-        const float4* xr = reinterpret_cast<const float4*>(x_in + (size_t)row * ldx);
 #pragma unroll
-        for (int c = 0; c < NV4; ++c) v[i][c] = xr[cidx[c]];
+        for (int c = 0; c < NV4; ++c) v[i][c] = load_resid4<XFIX>(x_in, (size_t)row * ldx, cidx[c], xcs);
 #pragma unroll
         for (int s = 0; s < NSPLIT; ++s) {
             const float4* pr = reinterpret_cast<const float4*>(parts + (size_t)s * split_stride + (size_t)row * ldp);
@@ -431,6 +475,7 @@ __global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restri
         bv[c] = reinterpret_cast<const float4*>(beta)[cidx[c]];
         rb[c] = res_bias ? reinterpret_cast<const float4*>(res_bias)[cidx[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    after_loads();
 
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
@@ -454,6 +499,11 @@ __global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restri
             for (int c = 0; c < NV4; ++c)
                 if (valid[c]) reinterpret_cast<float4*>(x_out + (size_t)row * ldx)[cidx[c]] = v[i][c];
         }
+        if (v_lds != nullptr) {
+#pragma unroll
+            for (int c = 0; c < NV4; ++c)
+                if (valid[c]) reinterpret_cast<float4*>(v_lds + (size_t)row * K)[cidx[c]] = v[i][c];
+        }
         const float mean = wave_sum(s) / (float)K;
         float ss = 0.f;
 #pragma unroll
@@ -476,6 +526,40 @@ __global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restri
             }
         }
     }
+}
+
+template <int EPI, int NSPLIT, int NV4, int RPW, int KBW, bool XFIX>
+__global__ __launch_bounds__(256) void skinny_addln_kernel(const void* __restrict__ x_in, float* __restrict__ x_out,
+                                                         int ldx, const float* __restrict__ parts, int ldp,
+                                                         long long split_stride, const float* __restrict__ res_bias,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         float eps, const bf16_t* __restrict__ Wsh, int M, int N, int K,
+                                                         GemmEpi ep, uint4* __restrict__ zero_buf, int zero_chunks,
+                                                         long long xcs) {
+    constexpr int NW = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int ng = blockIdx.x;
+    const int nkb = K >> 5;
+    const int per = (nkb + NW - 1) / NW;
+    const int kb0 = wave * per < nkb ? wave * per : nkb;
+    const int nk = (kb0 + per < nkb ? kb0 + per : nkb) - kb0;
+    const int kbl = nk > 0 ? kb0 : 0;
+    const int last = nk > 0 ? nk - 1 : 0;
+    const int g = lane >> 4, fr = lane & 15;
+    const int row_bytes = K * 2 + 16;
+
+    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wsh) + ((size_t)ng * nkb + kbl) * 64 + lane;
+    bf16x8_t b[KBW];
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
+    // the fixed-point accumulator the following fused MLP adds into starts from zero (grid-stride)
+    if (zero_buf != nullptr)
+        for (int z = blockIdx.x * 256 + threadIdx.x; z < zero_chunks; z += gridDim.x * 256) zero_buf[z] = make_uint4(0u, 0u, 0u, 0u);
+
+    addln_rows_lds<NSPLIT, NV4, RPW, XFIX>(x_in, x_out, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, M, K,
+                                           smem, row_bytes, xcs);
     __syncthreads();
 
     f32x4_t acc[1] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}};
@@ -495,46 +579,61 @@ __global__ __launch_bounds__(256) void skinny_addln_kernel(const float* __restri
     skinny_store<EPI, 1>(acc, M, ng * 16 + fr, g, ep);
 }
 
-template <int EPI, int NSPLIT, int NV4, int RPW>
-static hipError_t launch_addln(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
-                               const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M,
-                               int N, int K, const GemmEpi& ep, hipStream_t stream) {
+// launch arguments shared by every instantiation of the fused add+LN kernels
+struct AddlnArgs {
+    const void* x_in;
+    float* x_out;
+    int ldx;
+    const float* parts;
+    int ldp;
+    long long sstride;
+    const float* rbias;
+    const float* g;
+    const float* b;
+    float eps;
+    const bf16_t* W;
+    int M, N, K;
+    uint4* zero_buf;
+    int zero_chunks;
+    long long xcs;  // copy stride of a fixed-point x_in (elements)
+};
+
+template <int EPI, int NSPLIT, int NV4, int RPW, bool XFIX>
+static hipError_t launch_addln(const AddlnArgs& a, const GemmEpi& ep, hipStream_t stream) {
     constexpr int KBW = NV4 <= 2 ? 4 : (NV4 <= 4 ? 8 : (NV4 == 5 ? 12 : 16));  // >= K/32/4 for K <= 256 * NV4
-    const size_t lds = (size_t)16 * (K * 2 + 16);
-    hipLaunchKernelGGL((skinny_addln_kernel<EPI, NSPLIT, NV4, RPW, KBW>), dim3(N / 16), dim3(256), lds, stream, x_in,
-                       x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep);
+    const size_t lds = (size_t)16 * (a.K * 2 + 16);
+    hipLaunchKernelGGL((skinny_addln_kernel<EPI, NSPLIT, NV4, RPW, KBW, XFIX>), dim3(a.N / 16), dim3(256), lds, stream,
+                       a.x_in, a.x_out, a.ldx, a.parts, a.ldp, a.sstride, a.rbias, a.g, a.b, a.eps, a.W, a.M, a.N, a.K,
+                       ep, a.zero_buf, a.zero_chunks, a.xcs);
     return hipGetLastError();
 }
 
-template <int EPI, int NSPLIT, int NV4>
-static hipError_t addln_rpw(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
-                            const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M, int N,
-                            int K, const GemmEpi& ep, hipStream_t stream) {
-    if (M <= 4) return launch_addln<EPI, NSPLIT, NV4, 1>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+template <int EPI, int NSPLIT, int NV4, bool XFIX = false>
+static hipError_t addln_rpw(const AddlnArgs& a, const GemmEpi& ep, hipStream_t stream) {
+    if (a.M <= 4) return launch_addln<EPI, NSPLIT, NV4, 1, XFIX>(a, ep, stream);
     if constexpr (NV4 <= 4 && NSPLIT <= 4) {
-        if (M <= 8) return launch_addln<EPI, NSPLIT, NV4, 2>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        if (a.M <= 8) return launch_addln<EPI, NSPLIT, NV4, 2, XFIX>(a, ep, stream);
     }
     return hipErrorInvalidValue;
 }
 
 template <int EPI, int NSPLIT>
-static hipError_t addln_nv4(const float* x_in, float* x_out, int ldx, const float* parts, int ldp, long long sstride,
-                            const float* rbias, const float* g, const float* b, float eps, const bf16_t* W, int M, int N,
-                            int K, const GemmEpi& ep, hipStream_t stream) {
+static hipError_t addln_nv4(const AddlnArgs& a, const GemmEpi& ep, hipStream_t stream) {
+    const int K = a.K;
     if constexpr (NSPLIT > 4) {  // per-head slabs of the fused attention + out-projection (M <= 4, K <= 1024)
         switch ((K / 4 + 63) / 64) {
-            case 3: return addln_rpw<EPI, NSPLIT, 3>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-            case 4: return addln_rpw<EPI, NSPLIT, 4>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+            case 3: return addln_rpw<EPI, NSPLIT, 3>(a, ep, stream);
+            case 4: return addln_rpw<EPI, NSPLIT, 4>(a, ep, stream);
             default: return hipErrorInvalidValue;
         }
     }
     switch ((K / 4 + 63) / 64) {
-        case 1: return addln_rpw<EPI, NSPLIT, 1>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-        case 2: return addln_rpw<EPI, NSPLIT, 2>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-        case 3: return addln_rpw<EPI, NSPLIT, 3>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-        case 4: return addln_rpw<EPI, NSPLIT, 4>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-        case 5: return addln_rpw<EPI, NSPLIT, 5>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
-        case 7: return addln_rpw<EPI, NSPLIT, 7>(x_in, x_out, ldx, parts, ldp, sstride, rbias, g, b, eps, W, M, N, K, ep, stream);
+        case 1: return addln_rpw<EPI, NSPLIT, 1>(a, ep, stream);
+        case 2: return addln_rpw<EPI, NSPLIT, 2>(a, ep, stream);
+        case 3: return addln_rpw<EPI, NSPLIT, 3>(a, ep, stream);
+        case 4: return addln_rpw<EPI, NSPLIT, 4>(a, ep, stream);
+        case 5: return addln_rpw<EPI, NSPLIT, 5>(a, ep, stream);
+        case 7: return addln_rpw<EPI, NSPLIT, 7>(a, ep, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -546,14 +645,26 @@ extern "C" int dlms_skinny_addln_max_rows(int K) {
     return nv4 <= 4 ? 8 : 4;
 }
 
-extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const float* x_in, float* x_out, int ldx, const float* parts,
+// xfix: x_in is the int64 fixed-point residual a fused MLP left (QKV, no slabs only); zero_buf (when
+// given): zero_chunks 16-B chunks cleared for the fused MLP that follows (grid-stride over all blocks)
+extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const void* x_in, float* x_out, int ldx, const float* parts,
                                              int ldp, long long split_stride, int nsplit, const float* res_bias,
                                              const float* gamma, const float* beta, float eps, const void* Wsh, int M,
-                                             int N, int K, const GemmEpi* ep, hipStream_t stream) {
+                                             int N, int K, const GemmEpi* ep, int xfix, long long xcs, void* zero_buf,
+                                             int zero_chunks, hipStream_t stream) {
     if (M <= 0 || M > dlms_skinny_addln_max_rows(K) || N % 16) return hipErrorInvalidValue;
-    const bf16_t* W = reinterpret_cast<const bf16_t*>(Wsh);
-#define ADDLN(E, NS) \
-    return addln_nv4<E, NS>(x_in, x_out, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, W, M, N, K, *ep, stream)
+    if (xfix && (epi != SK_QKV || nsplit != 0 || x_out != nullptr)) return hipErrorInvalidValue;
+    const AddlnArgs a{x_in, x_out, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps,
+                      reinterpret_cast<const bf16_t*>(Wsh), M, N, K, reinterpret_cast<uint4*>(zero_buf),
+                      zero_buf ? zero_chunks : 0, xcs};
+    if (xfix) {
+        switch ((K / 4 + 63) / 64) {
+            case 3: return addln_rpw<SK_QKV, 0, 3, true>(a, *ep, stream);
+            case 4: return addln_rpw<SK_QKV, 0, 4, true>(a, *ep, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
+#define ADDLN(E, NS) return addln_nv4<E, NS>(a, *ep, stream)
 #define ADDLN_EPI(E)                    \
     switch (nsplit) {                   \
         case 0: ADDLN(E, 0);            \
@@ -570,6 +681,225 @@ extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const float* x_in, float* 
     }
 #undef ADDLN_EPI
 #undef ADDLN
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused MLP of the latency path (TP=1, M <= 4 * RPW rows): workgroup j owns intermediate columns
+// [16 j, 16 j + 16) of F = 4d (F / 16 workgroups, 4 waves):
+//
+//   v   = x_in + res_bias + sum_s parts[s]          (x_in f32 or fixed point; parts = attention slabs)
+//   h   = bf16(gelu(bf16(LN2(v)) . W_fc[16j..16j+16)^T + b_fc))        MFMA, K split over the waves
+//   out = h . W_p[:, 16j..16j+16)^T  (+ v + b_p in workgroup 0)        VALU, 16-deep dot per column
+//   r_out += fix(out)                                                  64-bit integer atomics
+//
+// It replaces [add+LN2+c_fc kernel] -> [c_proj kernel]: one kernel boundary and one dependent round
+// trip (the c_proj kernel's h read) fewer per layer.  Every weight byte (W_fc fragments and the
+// workgroup's contiguous 16-column W_p slice, Wp_sl [F/16][d][16]) is in flight before the
+// activation loads.  r_out (int64 fixed point, see DLMS_FIX_SCALE) must be zero on entry: the QKV
+// kernel of the same layer clears it.  Atomic traffic is M * d * 8 B per workgroup, so the engine
+// uses this kernel only at the smallest batches.
+typedef __attribute__((address_space(3))) void sk_lds_void_t;
+typedef __attribute__((address_space(1))) void sk_glob_void_t;
+
+template <int NSPLIT, int NV4, int RPW, int KBW, int NC, bool XFIX>
+__global__ __launch_bounds__(256) void skinny_mlp_kernel(
+    const void* __restrict__ x_in, int ldx, const float* __restrict__ parts, int ldp, long long split_stride,
+    const float* __restrict__ res_bias, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    const bf16_t* __restrict__ Wfc_sh, const float* __restrict__ b_fc, const bf16_t* __restrict__ Wp_sl,
+    const float* __restrict__ b_p, unsigned long long* __restrict__ r_out, int ldr, long long rcs, long long xcs, int M,
+    int K) {
+    constexpr int NW = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float hs[16][16];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int ng = blockIdx.x;
+    const int nkb = K >> 5;
+    const int per = (nkb + NW - 1) / NW;
+    const int kb0 = wave * per < nkb ? wave * per : nkb;
+    const int nk = (kb0 + per < nkb ? kb0 + per : nkb) - kb0;
+    const int kbl = nk > 0 ? kb0 : 0;
+    const int last = nk > 0 ? nk - 1 : 0;
+    const int g = lane >> 4, fr = lane & 15;
+    const int row_bytes = K * 2 + 16;
+
+    // (0) weights first: W_fc B fragments into registers; the workgroup's contiguous W_p slice
+    //     (K * 32 B) straight into LDS by LDS-DMA (no staging registers, lands under the LayerNorm);
+    //     the c_proj bias for this thread's output columns
+    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wfc_sh) + ((size_t)ng * nkb + kbl) * 64 + lane;
+    bf16x8_t b[KBW];
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
+    const int img_bytes = (16 * row_bytes + 1023) & ~1023;
+    char* wp_lds = smem + img_bytes;                       // [K][16] bf16
+    float* v_lds = reinterpret_cast<float*>(wp_lds + K * 32);  // block 0: [M][K] f32 residual rows
+    // K = 256 NC: K * 32 B = 8 NC KiB-pieces, 2 NC per wave (a compile-time count, so the LayerNorm's
+    // wait for the activation loads issued before them is a counted vmcnt, not a drain)
+    const char* wp_src = reinterpret_cast<const char*>(Wp_sl + (size_t)ng * K * 16) + lane * 16;
+    auto issue_wp = [&]() {
+#pragma unroll
+        for (int q = 0; q < 2 * NC; ++q) {
+            const int pc = wave + NW * q;
+            __builtin_amdgcn_global_load_lds((sk_glob_void_t*)(wp_src + pc * 1024), (sk_lds_void_t*)(wp_lds + pc * 1024),
+                                             16, 0, 0);
+        }
+    };
+    float bp[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        const int n = tid + 256 * i;
+        bp[i] = (blockIdx.x == 0 && n < K) ? b_p[n] : 0.f;
+    }
+
+    // (1) residual rows -> LN2 -> LDS image (block 0 also keeps v); (2) c_fc slice on MFMA
+    addln_rows_lds<NSPLIT, NV4, RPW, XFIX>(x_in, nullptr, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, M,
+                                           K, smem, row_bytes, xcs, blockIdx.x == 0 ? v_lds : nullptr, issue_wp);
+    __syncthreads();
+    f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KBW; ++u) {
+        if (u >= nk) continue;
+        const bf16x8_t av = lds_a_frag(smem, row_bytes, fr, kb0 + u, g);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b[u], acc, 0, 0, 0);
+    }
+    __syncthreads();  // LN image no longer read: reuse it for the fixed-order K-slice reduction
+    float* red = reinterpret_cast<float*>(smem);
+    if (wave > 0) *reinterpret_cast<f32x4_t*>(red + ((size_t)wave * 64 + lane) * 4) = acc;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the W_p DMA has landed ...
+    __syncthreads();                                  // ... and every other wave's
+    if (wave == 0) {
+#pragma unroll
+        for (int s = 1; s < NW; ++s) acc += *reinterpret_cast<const f32x4_t*>(red + ((size_t)s * 64 + lane) * 4);
+        const float bb = b_fc[ng * 16 + fr];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)  // bf16 rounding: the same operand the unfused c_proj reads
+            hs[g * 4 + r][fr] = bf16_to_f32(f32_to_bf16(gelu_tanh(acc[r] + bb)));
+    }
+    __syncthreads();
+
+    // (3) c_proj slice: thread t owns output columns (t + 256 i + rot) mod K; fixed-order 16-deep dot
+    //     per row.  rot staggers the workgroups' column order so their atomics to one address do not
+    //     arrive together (same-address atomics serialise at the memory side)
+    unsigned long long* rc = r_out + (size_t)(blockIdx.x % DLMS_FIX_COPIES) * rcs;
+    const int rot = (int)((blockIdx.x / DLMS_FIX_COPIES) * 64 % K);
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        int n = tid + 256 * i;
+        if (n >= K) continue;
+        n = n + rot < K ? n + rot : n + rot - K;
+        float w[16];
+        unpack8(*reinterpret_cast<const uint4*>(wp_lds + n * 32), w);
+        unpack8(*reinterpret_cast<const uint4*>(wp_lds + n * 32 + 16), w + 8);
+        for (int m = 0; m < M; ++m) {
+            float o = 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) o = fmaf(hs[m][k], w[k], o);
+            if (blockIdx.x == 0) o += v_lds[m * K + n] + bp[i];  // the residual and the c_proj bias, once
+            atomicAdd(rc + (size_t)m * ldr + n, f32_to_fix(o));
+        }
+    }
+}
+
+template <int NSPLIT, int NV4, int RPW, int NC, bool XFIX>
+static hipError_t launch_mlp(const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
+                             const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
+                             const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* r_out, int ldr,
+                             long long rcs, long long xcs, int M, int K, int F, hipStream_t stream) {
+    constexpr int KBW = NV4 <= 2 ? 4 : 8;  // >= K/32/4 for K <= 256 * NV4 (NV4 <= 4)
+    // LN image (1-KiB aligned) + W_p slice + block 0's residual rows
+    const size_t lds = (((size_t)16 * (K * 2 + 16) + 1023) & ~(size_t)1023) + (size_t)K * 32 + (size_t)4 * RPW * K * 4;
+    static bool attr_set = false;
+    if (!attr_set && lds > 65536) {
+        // (the kernel's static LDS comes on top: ask for what the largest K of this instantiation needs)
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_mlp_kernel<NSPLIT, NV4, RPW, KBW, NC, XFIX>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((skinny_mlp_kernel<NSPLIT, NV4, RPW, KBW, NC, XFIX>), dim3(F / 16), dim3(256), lds, stream, x_in,
+                       ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, r_out, ldr, rcs, xcs, M, K);
+    return hipGetLastError();
+}
+
+// x_in: f32 (xfix = 0) or int64 fixed point [M][ldx]; parts: nsplit (0 or 4) f32 slabs; Wfc_sh:
+// shuffle_weight(W_fc) [F/16][K/32][64][8]; Wp_sl [F/16][K][16]; r_out int64 [M][ldr], zeroed.
+extern "C" int dlms_fix_copies() { return DLMS_FIX_COPIES; }
+
+// r_out / a fixed-point x_in: DLMS_FIX_COPIES copies [copy][M][ld], copy strides rcs / xcs (elements)
+extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long long xcs, const float* parts, int ldp,
+                                      long long split_stride, int nsplit, const float* res_bias, const float* gamma,
+                                      const float* beta, float eps, const void* Wfc_sh, const float* b_fc,
+                                      const void* Wp_sl, const float* b_p, void* r_out, int ldr, long long rcs, int M,
+                                      int K, int F, hipStream_t stream) {
+    if (M <= 0 || M > 8 || K % 256 || K > 1024 || F % 16 || F <= 0) return hipErrorInvalidValue;
+    if (nsplit != 0 && nsplit != 4) return hipErrorInvalidValue;
+    const bf16_t* Wf = reinterpret_cast<const bf16_t*>(Wfc_sh);
+    const bf16_t* Wp = reinterpret_cast<const bf16_t*>(Wp_sl);
+    unsigned long long* R = reinterpret_cast<unsigned long long*>(r_out);
+#define MLP_GO(NS, NV, RPW_, NC_, XF) \
+    return launch_mlp<NS, NV, RPW_, NC_, XF>(x_in, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, Wf, b_fc, \
+                                            Wp, b_p, R, ldr, rcs, xcs, M, K, F, stream)
+#define MLP_RPW(NS, NV, NC_, XF) \
+    if (M <= 4) MLP_GO(NS, NV, 1, NC_, XF); else MLP_GO(NS, NV, 2, NC_, XF);
+#define MLP_X(NS, NV, NC_) \
+    if (xfix) { MLP_RPW(NS, NV, NC_, true) } else { MLP_RPW(NS, NV, NC_, false) }
+    switch (K) {
+        case 768:
+            if (nsplit == 4) { MLP_X(4, 3, 3) } else { MLP_X(0, 3, 3) }
+        case 1024:
+            if (nsplit == 4) { MLP_X(4, 4, 4) } else { MLP_X(0, 4, 4) }
+        default: return hipErrorInvalidValue;
+    }
+#undef MLP_X
+#undef MLP_RPW
+#undef MLP_GO
+}
+
+// Final LayerNorm of the fixed-point residual (ln_f after a fused MLP): one wave per row -> bf16.
+__global__ __launch_bounds__(64) void ln_fix_kernel(const long long* __restrict__ x, int ldx, long long xcs,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float eps, bf16_t* __restrict__ out, int ldo, int K) {
+    const int lane = threadIdx.x;
+    const int row = blockIdx.x;
+    const int nv = K >> 2;
+    float4 v[SK_MAX_LN_V4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < SK_MAX_LN_V4; ++i) {
+        const int c = lane + 64 * i;
+        v[i] = c < nv ? load_resid4<true>(x, (size_t)row * ldx, c, xcs) : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) / (float)K;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < SK_MAX_LN_V4; ++i) {
+        if (lane + 64 * i < nv) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+            ss += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)K + eps);
+#pragma unroll
+    for (int i = 0; i < SK_MAX_LN_V4; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nv) {
+            const float4 gg = reinterpret_cast<const float4*>(gamma)[c], bb = reinterpret_cast<const float4*>(beta)[c];
+            uint2 p;
+            p.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+            p.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+            *reinterpret_cast<uint2*>(out + (size_t)row * ldo + 4 * c) = p;
+        }
+    }
+}
+
+extern "C" hipError_t dlms_ln_fix(const void* x, int ldx, long long xcs, const float* gamma, const float* beta, float eps, void* out,
+                                  int ldo, int M, int K, hipStream_t stream) {
+    if (M <= 0 || K % 4 || K > 64 * 4 * SK_MAX_LN_V4 || ldx % 2 || ldo % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ln_fix_kernel, dim3(M), dim3(64), 0, stream, reinterpret_cast<const long long*>(x), ldx, xcs, gamma,
+                       beta, eps, reinterpret_cast<bf16_t*>(out), ldo, K);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -61,7 +61,8 @@ def _assert_teacher_forced(model, outs, prompts, eps=0.05, min_decisive=0.7):
     assert total > 0 and decisive >= min_decisive * total, (decisive, total)
 
 
-@pytest.mark.parametrize("name,batch", [("gpt2-tiny", 3), ("gpt2", 3), ("gpt2", 8), ("gpt2", 24), ("gpt2-medium", 2)])
+@pytest.mark.parametrize("name,batch", [("gpt2-tiny", 3), ("gpt2", 1), ("gpt2", 3), ("gpt2", 8), ("gpt2", 24),
+                                        ("gpt2-medium", 1), ("gpt2-medium", 2)])
 def test_generate_matches_reference_tokens(name, batch):
     """bf16 engine vs fp32 oracle, margin-aware and exact: batch 3/8 run the latency path
     (fused add+LN skinny GEMMs, split-K attention), 24 the tiled path."""
@@ -92,6 +93,28 @@ def test_latency_path_matches_tiled_path():
     ref = GPT2Reference(cfg, w, device="cuda")
     _assert_teacher_forced(ref, fast.generate(prompts), prompts)
     _assert_teacher_forced(ref, slow.generate(prompts), prompts)
+
+
+@pytest.mark.parametrize("name", ["gpt2", "gpt2-medium"])
+def test_fused_mlp_batch1(name, monkeypatch):
+    """Batch 1 runs LN2 -> c_fc -> GELU -> c_proj as one kernel into the int64 fixed-point residual:
+    exact under the margin rule against the fp32 oracle, identical across graph replay / eager and
+    across repeated runs (integer atomics), and tracking the unfused path."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+    from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference
+
+    cfg, w = _setup(name)
+    prompts = _prompts(cfg, [13], seed=21)
+    fused = HipGPT2Engine(cfg, w, max_batch=1, max_length=64)
+    assert fused.fused_mlp and fused.xr is not None
+    a = fused.generate(prompts)
+    assert fused.generate(prompts) == a
+    assert HipGPT2Engine(cfg, w, max_batch=1, max_length=64, use_graph=False).generate(prompts) == a
+    _assert_teacher_forced(GPT2Reference(cfg, w, device="cuda"), a, prompts)
+    monkeypatch.setenv("DLMS_FUSED_MLP", "0")
+    plain = HipGPT2Engine(cfg, w, max_batch=1, max_length=64)
+    assert not plain.fused_mlp
+    _assert_teacher_forced(GPT2Reference(cfg, w, device="cuda"), plain.generate(prompts), prompts)
 
 
 def test_graph_replay_equals_eager():

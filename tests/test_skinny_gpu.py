@@ -351,6 +351,110 @@ def test_skinny_addln_qkv(M):
         torch.testing.assert_close(vc[s, :, p].float().reshape(-1), z[r, 2 * D:], atol=3e-2, rtol=2e-2)
 
 
+def _to_fix(x):
+    """f32 [M, K] -> fixed point [fix_copies(), M, K], spread over the copies (readers must sum them)."""
+    from distributed_lms_raft_llm_amd import ops
+
+    C = ops.fix_copies()
+    total = torch.round(x.double() * ops.FIX_SCALE).to(torch.int64)
+    share = total // C
+    out = share.unsqueeze(0).repeat(C, 1, 1)
+    out[0] += total - share * C
+    return out.contiguous()
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 8])
+@pytest.mark.parametrize("K", [768, 1024])
+@pytest.mark.parametrize("nsplit,xfix", [(4, False), (4, True), (0, True)])
+def test_skinny_mlp(M, K, nsplit, xfix):
+    """Fused MLP: r_out += fix(v + gelu(LN(v) W_fc^T + b_fc) W_p^T + b_p), v = x + res_bias + sum(parts),
+    against fp32 (with the same bf16 roundings of LN(v) and h), and bit-identical over repeated launches
+    (the workgroups' 64-bit integer atomics commute)."""
+    ops = _ops()
+    F = 4 * K
+    x = _rand(M, K, seed=201, dtype=torch.float32) * 2
+    parts = _rand(4, M, K, seed=202, dtype=torch.float32) * 0.5
+    rb = _rand(K, seed=203, dtype=torch.float32)
+    g, b = _rand(K, seed=204, dtype=torch.float32), _rand(K, seed=205, dtype=torch.float32)
+    w_fc = _rand(F, K, scale=0.05, seed=206)
+    b_fc = _rand(F, seed=207, dtype=torch.float32) * 0.1
+    w_p = _rand(K, F, scale=0.03, seed=208)
+    b_p = _rand(K, seed=209, dtype=torch.float32) * 0.1
+    x_in = _to_fix(x) if xfix else x
+    x_used = ops.fix_to_float(x_in) if xfix else x
+    w_fc_sh, w_p_sl = ops.shuffle_weight(w_fc), ops.slice_cproj(w_p)
+    outs = []
+    for _ in range(3):
+        r = torch.zeros(ops.fix_copies(), M, K, dtype=torch.int64, device=DEV)
+        ops.skinny_mlp(x_in, g, b, 1e-5, w_fc_sh, b_fc, w_p_sl, b_p, r, parts=parts if nsplit else None,
+                       nsplit=nsplit, res_bias=rb)
+        outs.append(r)
+    assert all(torch.equal(outs[0], o) for o in outs[1:]), "fixed-point accumulation must be order-independent"
+    v = x_used + rb + parts[:nsplit].sum(0)
+    h = _ln_ref(v, g, b, 1e-5).to(torch.bfloat16).float()
+    ff = torch.nn.functional.gelu(h @ w_fc.float().t() + b_fc, approximate="tanh").to(torch.bfloat16).float()
+    ref = v + ff @ w_p.float().t() + b_p
+    torch.testing.assert_close(ops.fix_to_float(outs[0]), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_skinny_mlp_adds_into_accumulator():
+    """r_out is accumulated into, not overwritten: a pre-set value shows up in the result."""
+    ops = _ops()
+    M, K = 1, 768
+    x = _rand(M, K, seed=211, dtype=torch.float32)
+    g, b = _rand(K, seed=212, dtype=torch.float32), _rand(K, seed=213, dtype=torch.float32)
+    w_fc, w_p = _rand(4 * K, K, scale=0.05, seed=214), _rand(K, 4 * K, scale=0.03, seed=215)
+    b_fc, b_p = torch.zeros(4 * K, device=DEV), torch.zeros(K, device=DEV)
+    args = (g, b, 1e-5, ops.shuffle_weight(w_fc), b_fc, ops.slice_cproj(w_p), b_p)
+    C = ops.fix_copies()
+    r0 = torch.zeros(C, M, K, dtype=torch.int64, device=DEV)
+    ops.skinny_mlp(x, *args, r0)
+    r1 = torch.full((C, M, K), 5 << 32, dtype=torch.int64, device=DEV)
+    ops.skinny_mlp(x, *args, r1)
+    assert torch.equal(r1.sum(0) - r0.sum(0), torch.full_like(r0[0], C * (5 << 32)))
+
+
+@pytest.mark.parametrize("M", [1, 3])
+def test_skinny_addln_qkv_fixed_point_and_zero(M):
+    """QKV from the int64 fixed-point residual (the fused MLP's output) equals QKV from the same
+    residual in f32, and the kernel clears the side buffer it is handed."""
+    ops = _ops()
+    H, T, S = 12, 20, 16
+    D = 64 * H
+    x = _rand(M, D, seed=221, dtype=torch.float32) * 3
+    xf = _to_fix(x)
+    x32 = ops.fix_to_float(xf)
+    g, b = _rand(D, seed=222, dtype=torch.float32), _rand(D, seed=223, dtype=torch.float32)
+    w = ops.shuffle_weight(_rand(3 * D, D, scale=0.05, seed=224))
+    bias = _rand(3 * D, seed=225, dtype=torch.float32)
+    res = []
+    for xin in (x32, xf):
+        q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+        kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros_like(kc)
+        zero = torch.full((ops.fix_copies(), M, D), 123, dtype=torch.int64, device=DEV)
+        slot = torch.arange(M, dtype=torch.int32, device=DEV) * 2
+        pos = torch.arange(M, dtype=torch.int32, device=DEV) + 3
+        ops.skinny_addln_gemm(xin, w, ops.EPI_QKV, g, b, 1e-5, bias=bias, q_out=q, k_cache=kc, v_cache=vc,
+                              row_slot=slot, row_pos=pos, zero=zero)
+        assert int(zero.abs().sum()) == 0
+        res.append((q, kc, vc))
+    for a, c in zip(res[0], res[1]):
+        assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("M,K", [(1, 768), (3, 1024), (2, 1600)])
+def test_ln_fix(M, K):
+    ops = _ops()
+    x = _rand(M, K, seed=231, dtype=torch.float32) * 4 + 1
+    xf = _to_fix(x)
+    g, b = _rand(K, seed=232, dtype=torch.float32), _rand(K, seed=233, dtype=torch.float32)
+    out = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+    ops.ln_fix(xf, g, b, 1e-5, out)
+    ref = _ln_ref(ops.fix_to_float(xf), g, b, 1e-5)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=1e-2)
+
+
 # ---------------------------------------------------------------------------------------------
 # gemm_ps: LDS-resident activation panel + pre-shuffled weights (throughput path)
 # ---------------------------------------------------------------------------------------------
