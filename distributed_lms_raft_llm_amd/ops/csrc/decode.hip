@@ -27,25 +27,25 @@ __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ toke
 // max over a row's partial argmax keys, one wave per row (keys(b, p) = keys[b * sb + p * sp])
 __device__ __forceinline__ unsigned long long wave_key_max(const unsigned long long* __restrict__ keys, int b,
                                                            int nparts, long long sb, long long sp, int lane) {
-    // 8 independent loads in flight per lane per round (the LM head leaves ~800 partial keys per
-    // row at TP=1: a one-load-at-a-time loop paid ~13 dependent round trips per decode step)
+    // 16 independent loads in flight per lane per round: the LM head leaves ~800 partial keys per
+    // row at TP=1, one round trip (a one-load-at-a-time loop paid ~13 dependent round trips)
     unsigned long long best = 0ull;
-    for (int p0 = 0; p0 < nparts; p0 += 64 * 8) {
-        unsigned long long k[8];
+    for (int p0 = 0; p0 < nparts; p0 += 64 * 16) {
+        unsigned long long k[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 16; ++u) {
             const int p = p0 + lane + 64 * u;
             k[u] = p < nparts ? keys[(size_t)b * sb + (size_t)p * sp] : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) best = k[u] > best ? k[u] : best;
+        for (int u = 0; u < 16; ++u) best = k[u] > best ? k[u] : best;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long k = __shfl_xor(best, o, 64);
         best = k > best ? k : best;
     }
-    return best;
+    return best;  // identical in every lane
 }
 
 // argmax partials [B][nparts] -> one key per row (before the cross-rank all-gather under TP)
@@ -58,6 +58,8 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
     if (lane == 0) out[b] = best;
 }
 
+#define DU_MAXC 4  // 16-B embedding chunks per lane: D <= 64 * 4 * 8 = 2048
+
 // One wave per live sequence b.
 //   keys(b, p)   packed (ordered value, ~index) argmax keys: the LM head's per-column-tile
 //                partials (TP=1) or the all-gathered per-rank keys (TP>1); max over p
@@ -67,6 +69,9 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
 // Writes the next forward's token/position/kv-length for row b and its embedding into x.
 // slot_map (optional): key row i updates sequence slot slot_map[i] -- used when a prefill of new
 // requests lands in arbitrary free slots of a running continuous batch.
+// Dependency chain: everything that does not depend on the new token -- the row's length and stop
+// flag, its positional-embedding row, a finished row's last token -- is loaded together with the
+// keys, so the step pays two memory round trips (keys -> token embedding row), not five.
 __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long long* __restrict__ keys, int nparts,
                                                             long long sb, long long sp,
                                                             const int* __restrict__ slot_map, int* lens,
@@ -79,40 +84,53 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= B) return;
-    const unsigned long long best = wave_key_max(keys, i, nparts, sb, sp, lane);
     const int b = slot_map ? (int)dlms_idx(slot_map[i], n_slots, CHK_UPDATE_SLOT) : i;
-    int tok = 0, pos = 0;
+    // row state (every lane reads the same words: one request each)
+    const int len0 = (int)dlms_idx(lens[b], max_len + 1, CHK_UPDATE_LEN);
+    const int fin = finished[b];
+    // where a live row's token goes (a finished row may sit at len == max_len: not an index then)
+    const int live_len = fin ? 0 : (int)dlms_idx(len0, max_len, CHK_UPDATE_LEN);
+    int pos = fin ? len0 - 1 : live_len;  // (length after this step) - 1
+    pos = pos < 0 ? 0 : (pos < t_max - 1 ? pos : t_max - 1);
+    const int last_tok = fin ? out_tokens[(size_t)b * max_len + (len0 > 0 ? len0 - 1 : 0)] : 0;
+    const int nch = D >> 3;
+    uint4 pe[DU_MAXC];
+#pragma unroll
+    for (int u = 0; u < DU_MAXC; ++u) {
+        const int c = lane + 64 * u;
+        pe[u] = c < nch ? *reinterpret_cast<const uint4*>(wpe + (size_t)pos * D + c * 8) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const unsigned long long best = wave_key_max(keys, i, nparts, sb, sp, lane);
+
+    int tok;
+    if (!fin) {
+        // best == 0 means no shard produced a candidate (cannot happen for vocab >= 1); stay in
+        // bounds anyway by emitting EOS.
+        tok = best ? (int)(~(unsigned int)(best & 0xffffffffull)) : eos;
+        tok = (int)dlms_idx(tok, V, CHK_UPDATE_TOKEN);
+    } else {
+        tok = (int)dlms_idx(last_tok, V, CHK_UPDATE_TOKEN);
+    }
     if (lane == 0) {
-        int len = (int)dlms_idx(lens[b], max_len + 1, CHK_UPDATE_LEN);
-        if (!finished[b]) {
-            // best == 0 means no shard produced a candidate (cannot happen for vocab >= 1); stay in
-            // bounds anyway by emitting EOS.
-            tok = best ? (int)(~(unsigned int)(best & 0xffffffffull)) : eos;
-            tok = (int)dlms_idx(tok, V, CHK_UPDATE_TOKEN);
-            len = (int)dlms_idx(len, max_len, CHK_UPDATE_LEN);
-            out_tokens[(size_t)b * max_len + len] = tok;
-            seen[(size_t)b * seen_words + (tok >> 5)] |= 1u << (tok & 31);
-            len += 1;
-            lens[b] = len;
-            if (tok == eos || len >= max_len) finished[b] = 1;
-        } else {
-            tok = (int)dlms_idx(out_tokens[(size_t)b * max_len + (len > 0 ? len - 1 : 0)], V, CHK_UPDATE_TOKEN);
+        if (!fin) {
+            out_tokens[(size_t)b * max_len + live_len] = tok;
+            atomicOr(seen + (size_t)b * seen_words + (tok >> 5), 1u << (tok & 31));  // no read-back wait
+            lens[b] = live_len + 1;
+            if (tok == eos || live_len + 1 >= max_len) finished[b] = 1;
         }
-        pos = len - 1;
-        pos = pos < t_max - 1 ? pos : t_max - 1;
         cur_tok[b] = tok;
         cur_pos[b] = pos;
         cur_kvlen[b] = pos + 1;
     }
-    tok = __shfl(tok, 0, 64);
-    pos = __shfl(pos, 0, 64);
     const bf16_t* a = wte + (size_t)tok * D;
-    const bf16_t* p = wpe + (size_t)pos * D;
     float* o = x + (size_t)b * ldx;
-    for (int c = lane; c < D / 8; c += 64) {
+#pragma unroll
+    for (int u = 0; u < DU_MAXC; ++u) {
+        const int c = lane + 64 * u;
+        if (c >= nch) continue;
         float fa[8], fb[8];
         unpack8(*reinterpret_cast<const uint4*>(a + c * 8), fa);
-        unpack8(*reinterpret_cast<const uint4*>(p + c * 8), fb);
+        unpack8(pe[u], fb);
         reinterpret_cast<float4*>(o + c * 8)[0] = make_float4(fa[0] + fb[0], fa[1] + fb[1], fa[2] + fb[2], fa[3] + fb[3]);
         reinterpret_cast<float4*>(o + c * 8)[1] = make_float4(fa[4] + fb[4], fa[5] + fb[5], fa[6] + fb[6], fa[7] + fb[7]);
     }
@@ -131,7 +149,7 @@ extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int npa
                                          unsigned int* seen, int seen_words, int* cur_tok, int* cur_pos,
                                          int* cur_kvlen, const void* wte, const void* wpe, float* x, int ldx, int B,
                                          int D, int eos, int t_max, int n_slots, int V, hipStream_t stream) {
-    if (D % 8 != 0 || B <= 0 || nparts <= 0) return hipErrorInvalidValue;
+    if (D % 8 != 0 || D > 64 * DU_MAXC * 8 || B <= 0 || nparts <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, sp, slot_map,
                        lens, finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
                        reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, B, D, eos,
