@@ -22,6 +22,7 @@ No host round trip happens inside a step; the host only checks the stop flags ev
 """
 from __future__ import annotations
 
+import itertools
 import math
 import os
 import time
@@ -855,7 +856,7 @@ class HipGPT2Engine:
         # 1024-prompt admission used to spend ~20 ms of host time here with the GPU idle)
         lens_np = np.asarray(lens, dtype=np.int64)
         ends = np.cumsum(lens_np)
-        tok_np = np.fromiter((t for p in prompts for t in p), dtype=np.int64, count=R)
+        tok_np = np.fromiter(itertools.chain.from_iterable(prompts), dtype=np.int64, count=R)
         if tok_np.min() < 0 or tok_np.max() >= cfg.vocab_size:
             raise ValueError("prefill: token id out of range")
         pos_np = np.arange(R, dtype=np.int64) - np.repeat(ends - lens_np, lens_np)
@@ -1073,8 +1074,7 @@ class HipGPT2Engine:
             for i in range(0, n, self.max_batch):
                 out += self.generate(prompts[i: i + self.max_batch], max_length, repetition_penalty, stats)
             return out
-        prompts = [list(p) for p in prompts]
-        B = min(_bucket(n), self.max_batch)
+        B = min(_bucket(n), self.max_batch)  # (prompts are passthrough()'s normalised copies)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev2 = torch.cuda.Event(enable_timing=True)
@@ -1110,10 +1110,12 @@ class HipGPT2Engine:
             pending = (ev, slot)
         ev2.record()
         lens = self.lens[:n].cpu().tolist()
-        toks = self.out_tokens[:n].cpu().tolist()  # one conversion, not one per row
+        # one device->host copy, then numpy's list conversion (about half the host time of
+        # Tensor.tolist on 1024 x 150 ids), only up to each row's length
+        toks = self.out_tokens[:n].cpu().numpy()
         if self.xgmi is not None:
             self.xgmi.check()  # a timed-out peer barrier means these tokens are garbage
-        res = [toks[b][: lens[b]] for b in range(n)]
+        res = [toks[b, : lens[b]].tolist() for b in range(n)]
         if stats is not None:
             ev2.synchronize()
             stats.batch += n

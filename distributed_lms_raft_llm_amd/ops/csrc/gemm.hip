@@ -433,6 +433,10 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
             // tiles sit exactly at the CU's LDS-bandwidth : MFMA-rate balance)
             case 12: return launch_gemm_cfg<256, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             case 13: return launch_gemm_cfg<256, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            // few-row LM head: 32-row A tiles (a 64-row tile at batch 1 fills a third of every
+            // ring stage with clamped copies of the same row)
+            case 15: return launch_gemm_cfg<32, 128, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 16: return launch_gemm_cfg<32, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
             default: break;
         }
     }
@@ -479,6 +483,11 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     }
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
         return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    // few-row LM head (latency path, B <= 32): 32-row A tiles, so clamped copies of the few real rows
+    // take a fifth of each ring stage instead of a third (batch 1: 34.86 -> 34.46 ms per query,
+    // profiles/r2_lm_head_tiles_b1.txt)
+    if (EPI == EPI_ARGMAX && M <= 32 && N % 128 == 0 && N >= 8192)
+        return launch_gemm_cfg<32, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (N % 128 == 0 && N >= 8192) return launch_gemm_cfg<64, 128, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (M <= 64) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (t64 <= 400) return launch_gemm_cfg<64, 64, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);

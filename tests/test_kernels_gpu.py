@@ -153,7 +153,7 @@ def test_gemm_wide_model_tiles(epi, M, N, K):
     torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [37, 512])
+@pytest.mark.parametrize("M", [1, 5, 32, 37, 512])
 def test_gemm_argmax_penalty(M):
     """Fused penalty + argmax epilogue vs fp32.  The key buffer is pre-filled with huge stale keys,
     which a tile wider than 64 columns must zero in every 64-column group it covers (a narrower
