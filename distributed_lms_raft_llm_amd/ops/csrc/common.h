@@ -43,17 +43,50 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
     return r;
 }
 
+// Lane permute within 16-lane rows by DPP (a VALU operand modifier: no LDS round trip, unlike the
+// ds_bpermute_b32 that __shfl_xor compiles to -- six of those per reduction sat on the critical path
+// of every LayerNorm).  CTRL: 0xB1 quad_perm[1,0,3,2], 0x4E quad_perm[2,3,0,1], 0x141 row_half_mirror,
+// 0x140 row_mirror.
+template <int CTRL>
+__device__ __forceinline__ float dpp_perm(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float lane_value(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Full-wave reductions: butterflies inside each 16-lane row by DPP, then the four row results
+// combined in a fixed order from scalar registers (the same value in every lane, deterministic).
+// (-DDLMS_SHFL_REDUCE=1 builds the former ds_bpermute butterflies, for A/B runs)
+#if DLMS_SHFL_REDUCE
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
+#else
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp_perm<0xB1>(v);
+    v += dpp_perm<0x4E>(v);
+    v += dpp_perm<0x141>(v);
+    v += dpp_perm<0x140>(v);
+    return (lane_value(v, 0) + lane_value(v, 16)) + (lane_value(v, 32) + lane_value(v, 48));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp_perm<0xB1>(v));
+    v = fmaxf(v, dpp_perm<0x4E>(v));
+    v = fmaxf(v, dpp_perm<0x141>(v));
+    v = fmaxf(v, dpp_perm<0x140>(v));
+    return fmaxf(fmaxf(lane_value(v, 0), lane_value(v, 16)), fmaxf(lane_value(v, 32), lane_value(v, 48)));
+}
+#endif
 
 __device__ __forceinline__ float gelu_tanh(float x) {
     const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
