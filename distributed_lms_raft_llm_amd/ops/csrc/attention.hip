@@ -47,9 +47,7 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
 #pragma unroll
             for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
         }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
+        s = group8_sum(s);
         if (c == 0 && t < kvlen) sc[t] = s * scale;
     }
     __syncthreads();
@@ -87,7 +85,7 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        acc[j] += __shfl_xor(acc[j], 8, 64);
+        acc[j] += xor_lane(acc[j], 8);
         acc[j] += __shfl_xor(acc[j], 16, 64);
         acc[j] += __shfl_xor(acc[j], 32, 64);
     }
@@ -161,9 +159,7 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
             float s = 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
-            s += __shfl_xor(s, 1, 64);
-            s += __shfl_xor(s, 2, 64);
-            s += __shfl_xor(s, 4, 64);
+            s = group8_sum(s);
             const bool valid = t0 + u * 8 + g < kvlen;
             if (valid) {
                 const float m_new = fmaxf(m, s);
@@ -181,15 +177,15 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
     // merge the 8 key groups (lanes c, c+8, ..., c+56 hold partials of the same dims)
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = __shfl_xor(m, o, 64);
-        const float l_o = __shfl_xor(l, o, 64);
+        const float m_o = xor_lane(m, o);
+        const float l_o = xor_lane(l, o);
         const float m_n = fmaxf(m, m_o);
         const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
         const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
         l = l * a + l_o * b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float x_o = __shfl_xor(acc[j], o, 64);
+            const float x_o = xor_lane(acc[j], o);
             acc[j] = acc[j] * a + x_o * b;
         }
         m = m_n;
@@ -252,9 +248,7 @@ __global__ __launch_bounds__(256) void attn_persist_kernel(const bf16_t* __restr
                 float s = 0.f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
-                s += __shfl_xor(s, 1, 64);
-                s += __shfl_xor(s, 2, 64);
-                s += __shfl_xor(s, 4, 64);
+                s = group8_sum(s);
                 if (t0 + u * 8 + g < kvlen) {
                     const float m_new = fmaxf(m, s);
                     const float corr = exp2f(m - m_new);
@@ -270,15 +264,15 @@ __global__ __launch_bounds__(256) void attn_persist_kernel(const bf16_t* __restr
         }
 #pragma unroll
         for (int o = 8; o < 64; o <<= 1) {
-            const float m_o = __shfl_xor(m, o, 64);
-            const float l_o = __shfl_xor(l, o, 64);
+            const float m_o = xor_lane(m, o);
+            const float l_o = xor_lane(l, o);
             const float m_n = fmaxf(m, m_o);
             const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
             const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
             l = l * a + l_o * b;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float x_o = __shfl_xor(acc[j], o, 64);
+                const float x_o = xor_lane(acc[j], o);
                 acc[j] = acc[j] * a + x_o * b;
             }
             m = m_n;

@@ -52,6 +52,58 @@ __device__ __forceinline__ float dpp_perm(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_perm_u64(unsigned long long v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned int)v, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned int)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
+}
+
+// v from lane (lane ^ o): DPP for o in {1, 2, 8} (quad_perm [1,0,3,2] / [2,3,0,1], row_ror:8 -- the
+// same permutations, bit for bit), ds_bpermute otherwise.  o must fold to a constant.
+__device__ __forceinline__ float xor_lane(float v, int o) {
+    if (o == 1) return dpp_perm<0xB1>(v);
+    if (o == 2) return dpp_perm<0x4E>(v);
+    if (o == 8) return dpp_perm<0x128>(v);
+    return __shfl_xor(v, o, 64);
+}
+
+// Sum over aligned 8-lane groups, in every lane of the group: bit-identical to the xor 1, 2, 4
+// butterfly (after two steps every quad holds one value, so the half-row mirror pairs each lane
+// with the other quad exactly as xor 4 does), without an LDS round trip.
+__device__ __forceinline__ float group8_sum(float s) {
+    s += dpp_perm<0xB1>(s);
+    s += dpp_perm<0x4E>(s);
+    s += dpp_perm<0x141>(s);
+    return s;
+}
+
+// Max over each 16-lane row (xor 1, 2, 4, 8 butterfly by DPP; max is order-free)
+__device__ __forceinline__ unsigned long long row16_max_u64(unsigned long long k) {
+    unsigned long long o;
+    o = dpp_perm_u64<0xB1>(k); k = o > k ? o : k;
+    o = dpp_perm_u64<0x4E>(k); k = o > k ? o : k;
+    o = dpp_perm_u64<0x141>(k); k = o > k ? o : k;
+    o = dpp_perm_u64<0x128>(k); k = o > k ? o : k;
+    return k;
+}
+
+__device__ __forceinline__ unsigned long long lane_value_u64(unsigned long long v, int lane) {
+    const unsigned int lo = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)v, lane);
+    const unsigned int hi = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(v >> 32), lane);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// Max over the wave, the same value in every lane
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long k) {
+    k = row16_max_u64(k);
+    unsigned long long a = lane_value_u64(k, 0), b = lane_value_u64(k, 16);
+    const unsigned long long c = lane_value_u64(k, 32), d = lane_value_u64(k, 48);
+    a = b > a ? b : a;
+    a = c > a ? c : a;
+    return d > a ? d : a;
+}
+
 __device__ __forceinline__ float lane_value(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }

@@ -40,12 +40,7 @@ __device__ __forceinline__ unsigned long long wave_key_max(const unsigned long l
 #pragma unroll
         for (int u = 0; u < 16; ++u) best = k[u] > best ? k[u] : best;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long k = __shfl_xor(best, o, 64);
-        best = k > best ? k : best;
-    }
-    return best;  // identical in every lane
+    return wave_max_u64(best);  // identical in every lane
 }
 
 // argmax partials [B][nparts] -> one key per row (before the cross-rank all-gather under TP)

@@ -251,11 +251,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
                         ((unsigned long long)f32_ordered(v) << 32) | (unsigned long long)(~(unsigned int)gcol);
                     b = (gcol < ep.vocab && key > b) ? key : b;
                 }
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    const unsigned long long other = __shfl_xor(b, o, 64);
-                    b = other > b ? other : b;
-                }
+                b = row16_max_u64(b);  // max over the 16 lanes of this row
                 if ((lane & 15) == 0) sred[wn * BM + lr] = b;
             }
         }

@@ -270,11 +270,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 unsigned long long k = best[i][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    const unsigned long long other = __shfl_xor(k, o, 64);
-                    k = other > k ? other : k;
-                }
+                k = row16_max_u64(k);  // max over the 16 lanes of this row
                 const int row = m0 + 16 * i + 4 * g + r;
                 if (fr == 0 && row < M) ep.argmax_out[(size_t)row * ep.ldo + slot] = k;
             }

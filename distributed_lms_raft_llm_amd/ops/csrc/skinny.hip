@@ -252,11 +252,7 @@ __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const void* __rest
                     if ((bits >> (gcol & 31)) & 1u) v = v < 0.f ? v * ep.penalty : v / ep.penalty;
                     unsigned long long key =
                         valid ? (((unsigned long long)f32_ordered(v) << 32) | (unsigned long long)(~(unsigned int)gcol)) : 0ull;
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) {
-                        const unsigned long long other = __shfl_xor(key, o, 64);
-                        key = other > key ? other : key;
-                    }
+                    key = row16_max_u64(key);  // max over the 16 lanes of this row
                     if (fr == 0) kred[cgi][row] = key;
                 }
         }
@@ -969,9 +965,7 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
             float s = 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
-            s += __shfl_xor(s, 1, 64);
-            s += __shfl_xor(s, 2, 64);
-            s += __shfl_xor(s, 4, 64);
+            s = group8_sum(s);
             if (t0 + u * 8 + g < t_hi) {
                 const float m_new = fmaxf(m, s);
                 const float corr = exp2f(m - m_new);
@@ -987,15 +981,15 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
     }
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = __shfl_xor(m, o, 64);
-        const float l_o = __shfl_xor(l, o, 64);
+        const float m_o = xor_lane(m, o);
+        const float l_o = xor_lane(l, o);
         const float m_n = fmaxf(m, m_o);
         const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
         const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
         l = l * a + l_o * b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float x_o = __shfl_xor(acc[j], o, 64);
+            const float x_o = xor_lane(acc[j], o);
             acc[j] = acc[j] * a + x_o * b;
         }
         m = m_n;
@@ -1187,9 +1181,7 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(
                 float sc = 0.f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sc += qf[e] * kf[e];
-                sc += __shfl_xor(sc, 1, 64);
-                sc += __shfl_xor(sc, 2, 64);
-                sc += __shfl_xor(sc, 4, 64);
+                sc = group8_sum(sc);
                 if (t0 + u * 8 + g < t_hi) {
                     const float m_new = fmaxf(m, sc);
                     const float corr = exp2f(m - m_new);
@@ -1206,14 +1198,14 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(
     }
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = __shfl_xor(m, o, 64);
-        const float l_o = __shfl_xor(l, o, 64);
+        const float m_o = xor_lane(m, o);
+        const float l_o = xor_lane(l, o);
         const float m_n = fmaxf(m, m_o);
         const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
         const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
         l = l * a + l_o * b;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + __shfl_xor(acc[e], o, 64) * b;
+        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + xor_lane(acc[e], o) * b;
         m = m_n;
     }
     if (g == 0) {
@@ -1332,9 +1324,7 @@ __global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
             float sc = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) sc += qf[e] * kf[e];
-            sc += __shfl_xor(sc, 1, 64);
-            sc += __shfl_xor(sc, 2, 64);
-            sc += __shfl_xor(sc, 4, 64);
+            sc = group8_sum(sc);
             if (t0 + u * 8 + g < t_hi) {
                 const float m_new = fmaxf(m, sc);
                 const float corr = exp2f(m - m_new);
@@ -1350,14 +1340,14 @@ __global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
     }
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = __shfl_xor(m, o, 64);
-        const float l_o = __shfl_xor(l, o, 64);
+        const float m_o = xor_lane(m, o);
+        const float l_o = xor_lane(l, o);
         const float m_n = fmaxf(m, m_o);
         const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
         const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
         l = l * a + l_o * b;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + __shfl_xor(acc[e], o, 64) * b;
+        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + xor_lane(acc[e], o) * b;
         m = m_n;
     }
     if (g == 0) {
