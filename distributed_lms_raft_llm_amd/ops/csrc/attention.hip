@@ -86,8 +86,8 @@ __global__ __launch_bounds__(256) void row_attention_kernel(const bf16_t* __rest
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         acc[j] += xor_lane(acc[j], 8);
-        acc[j] += __shfl_xor(acc[j], 16, 64);
-        acc[j] += __shfl_xor(acc[j], 32, 64);
+        { float x_, y_; lane_pair(acc[j], 16, x_, y_); acc[j] = x_ + y_; }
+        { float x_, y_; lane_pair(acc[j], 32, x_, y_); acc[j] = x_ + y_; }
     }
     __syncthreads();  // red[] reuse
     if (kk == 0) {
@@ -177,16 +177,18 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
     // merge the 8 key groups (lanes c, c+8, ..., c+56 hold partials of the same dims)
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = xor_lane(m, o);
-        const float l_o = xor_lane(l, o);
-        const float m_n = fmaxf(m, m_o);
-        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
-        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
-        l = l * a + l_o * b;
+        float mx, my, lx, ly;  // (own, partner) or (lower, upper): the merge is symmetric
+        lane_pair(m, o, mx, my);
+        lane_pair(l, o, lx, ly);
+        const float m_n = fmaxf(mx, my);
+        const float a = mx == -INFINITY ? 0.f : exp2f(mx - m_n);
+        const float b = my == -INFINITY ? 0.f : exp2f(my - m_n);
+        l = lx * a + ly * b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float x_o = xor_lane(acc[j], o);
-            acc[j] = acc[j] * a + x_o * b;
+            float ax, ay;
+            lane_pair(acc[j], o, ax, ay);
+            acc[j] = ax * a + ay * b;
         }
         m = m_n;
     }
@@ -264,16 +266,18 @@ __global__ __launch_bounds__(256) void attn_persist_kernel(const bf16_t* __restr
         }
 #pragma unroll
         for (int o = 8; o < 64; o <<= 1) {
-            const float m_o = xor_lane(m, o);
-            const float l_o = xor_lane(l, o);
-            const float m_n = fmaxf(m, m_o);
-            const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
-            const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
-            l = l * a + l_o * b;
+            float mx, my, lx, ly;  // (own, partner) or (lower, upper): the merge is symmetric
+            lane_pair(m, o, mx, my);
+            lane_pair(l, o, lx, ly);
+            const float m_n = fmaxf(mx, my);
+            const float a = mx == -INFINITY ? 0.f : exp2f(mx - m_n);
+            const float b = my == -INFINITY ? 0.f : exp2f(my - m_n);
+            l = lx * a + ly * b;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float x_o = xor_lane(acc[j], o);
-                acc[j] = acc[j] * a + x_o * b;
+                float ax, ay;
+                lane_pair(acc[j], o, ax, ay);
+                acc[j] = ax * a + ay * b;
             }
             m = m_n;
         }
@@ -431,8 +435,8 @@ __global__ __launch_bounds__(256) void attn_tile_kernel(const bf16_t* __restrict
             sv[j] = v;
             mx = fmaxf(mx, v);
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        { float x_, y_; lane_pair(mx, 16, x_, y_); mx = fmaxf(x_, y_); }
+        { float x_, y_; lane_pair(mx, 32, x_, y_); mx = fmaxf(x_, y_); }
         const float m_new = fmaxf(m, mx);
         const bool none = m_new == -INFINITY;  // no valid key yet for this query
         const float corr = none ? 1.f : exp2f(m - m_new);
@@ -444,8 +448,8 @@ __global__ __launch_bounds__(256) void attn_tile_kernel(const bf16_t* __restrict
             psum += p;
             pa[j] = (short)f32_to_bf16(p);
         }
-        psum += __shfl_xor(psum, 16, 64);
-        psum += __shfl_xor(psum, 32, 64);
+        { float x_, y_; lane_pair(psum, 16, x_, y_); psum = x_ + y_; }
+        { float x_, y_; lane_pair(psum, 32, x_, y_); psum = x_ + y_; }
         l = l * corr + psum;
         m = m_new;
         // O rows are queries 4g + r: fetch their correction factors from lanes 4g + r

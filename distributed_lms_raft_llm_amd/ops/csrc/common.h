@@ -68,6 +68,30 @@ __device__ __forceinline__ float xor_lane(float v, int o) {
     return __shfl_xor(v, o, 64);
 }
 
+// This lane's value and its lane ^ o partner's, as (x, y): for o in {16, 32} from one gfx950
+// v_permlane{16,32}_swap (x = the lower row's / half's value, y = the upper's, the same pair in both
+// partner lanes), otherwise x = own, y = partner (xor_lane).  Callers combine x and y symmetrically
+// (sums, the online-softmax merge), which gives the same result as (own, partner) bit for bit.
+__device__ __forceinline__ void lane_pair(float v, int o, float& x, float& y) {
+#if DLMS_NO_PERMLANE  // A/B builds: the ds_bpermute exchange for every o
+    x = v;
+    y = xor_lane(v, o);
+    return;
+#endif
+    if (o == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        x = __uint_as_float(r[0]);
+        y = __uint_as_float(r[1]);
+    } else if (o == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        x = __uint_as_float(r[0]);
+        y = __uint_as_float(r[1]);
+    } else {
+        x = v;
+        y = xor_lane(v, o);
+    }
+}
+
 // Sum over aligned 8-lane groups, in every lane of the group: bit-identical to the xor 1, 2, 4
 // butterfly (after two steps every quad holds one value, so the half-row mirror pairs each lane
 // with the other quad exactly as xor 4 does), without an LDS round trip.

@@ -981,16 +981,18 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
     }
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = xor_lane(m, o);
-        const float l_o = xor_lane(l, o);
-        const float m_n = fmaxf(m, m_o);
-        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
-        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
-        l = l * a + l_o * b;
+        float mx, my, lx, ly;  // (own, partner) or (lower, upper): the merge is symmetric
+        lane_pair(m, o, mx, my);
+        lane_pair(l, o, lx, ly);
+        const float m_n = fmaxf(mx, my);
+        const float a = mx == -INFINITY ? 0.f : exp2f(mx - m_n);
+        const float b = my == -INFINITY ? 0.f : exp2f(my - m_n);
+        l = lx * a + ly * b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float x_o = xor_lane(acc[j], o);
-            acc[j] = acc[j] * a + x_o * b;
+            float ax, ay;
+            lane_pair(acc[j], o, ax, ay);
+            acc[j] = ax * a + ay * b;
         }
         m = m_n;
     }
@@ -1198,14 +1200,19 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(
     }
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = xor_lane(m, o);
-        const float l_o = xor_lane(l, o);
-        const float m_n = fmaxf(m, m_o);
-        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
-        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
-        l = l * a + l_o * b;
+        float mx, my, lx, ly;  // (own, partner) or (lower, upper): the merge is symmetric
+        lane_pair(m, o, mx, my);
+        lane_pair(l, o, lx, ly);
+        const float m_n = fmaxf(mx, my);
+        const float a = mx == -INFINITY ? 0.f : exp2f(mx - m_n);
+        const float b = my == -INFINITY ? 0.f : exp2f(my - m_n);
+        l = lx * a + ly * b;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + xor_lane(acc[e], o) * b;
+        for (int e = 0; e < 8; ++e) {
+            float ax, ay;
+            lane_pair(acc[e], o, ax, ay);
+            acc[e] = ax * a + ay * b;
+        }
         m = m_n;
     }
     if (g == 0) {
@@ -1340,14 +1347,19 @@ __global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
     }
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-        const float m_o = xor_lane(m, o);
-        const float l_o = xor_lane(l, o);
-        const float m_n = fmaxf(m, m_o);
-        const float a = m == -INFINITY ? 0.f : exp2f(m - m_n);
-        const float b = m_o == -INFINITY ? 0.f : exp2f(m_o - m_n);
-        l = l * a + l_o * b;
+        float mx, my, lx, ly;  // (own, partner) or (lower, upper): the merge is symmetric
+        lane_pair(m, o, mx, my);
+        lane_pair(l, o, lx, ly);
+        const float m_n = fmaxf(mx, my);
+        const float a = mx == -INFINITY ? 0.f : exp2f(mx - m_n);
+        const float b = my == -INFINITY ? 0.f : exp2f(my - m_n);
+        l = lx * a + ly * b;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = acc[e] * a + xor_lane(acc[e], o) * b;
+        for (int e = 0; e < 8; ++e) {
+            float ax, ay;
+            lane_pair(acc[e], o, ax, ay);
+            acc[e] = ax * a + ay * b;
+        }
         m = m_n;
     }
     if (g == 0) {
