@@ -279,6 +279,9 @@ class HipGPT2Engine:
         # integer atomics; ops.skinny_mlp) -- one launch and one dependent round trip fewer per layer
         self.fused_mlp = (self.ao_groups > 0 and cfg.n_embd in (768, 1024) and self.w.ffn_local == 4 * cfg.n_embd and
                           os.environ.get("DLMS_FUSED_MLP", "1") != "0")
+        # ... and up to this many rows (2-8: split attention + in-place out-projection into the
+        # fixed-point residual; each row adds 6 KB of atomics per MLP workgroup)
+        self.fused_mlp_rows = int(os.environ.get("DLMS_FUSED_MLP_ROWS", "2")) if self.fused_mlp else 0
         if self.fused_mlp:
             for lw in self.w.layers:
                 if lw.w_p_sl is None:
@@ -319,7 +322,8 @@ class HipGPT2Engine:
         # second residual buffer: the latency path's fused add+LN kernels advance x by ping-pong
         self.x2 = torch.zeros(min(B, 64), D, dtype=f32, device=dev)
         # the fused MLP's ping-pong int64 fixed-point residual (batch 1)
-        self.xr = torch.zeros(2, ops.fix_copies(), 1, D, dtype=torch.int64, device=dev) if self.fused_mlp else None
+        self.xr = (torch.zeros(2, ops.fix_copies(), max(1, min(self.fused_mlp_rows, B)), D, dtype=torch.int64, device=dev)
+                   if self.fused_mlp else None)
         # cross-workgroup split attention (few rows, long caches): partials + arrival counters
         self.attn_ws = ops.AttnSplitWorkspace(self.SPLIT_ATTN_MAX_PAIRS, 2, dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
@@ -672,7 +676,7 @@ class HipGPT2Engine:
                 self._all_reduce(self.parts[0, :B])
             return split
 
-        if inplace and self.fused_mlp and B == 1 and not r.part and not lo:
+        if inplace and self.fused_mlp and B <= max(1, self.fused_mlp_rows) and not r.part and not lo:
             self._decode_layers_fused_mlp(r, B)
             ops.ln_fix(self.xr[(len(self.w.layers) - 1) % 2, :, :B], self.w.lnf_g, self.w.lnf_b, eps, self.h[:B])
             self._lm_head_and_update(self.h[:B], B, penalty)
@@ -730,21 +734,29 @@ class HipGPT2Engine:
         self._lm_head_and_update(self.h[lo:hi], B, penalty, lo=lo)
 
     def _decode_layers_fused_mlp(self, r, B: int):
-        """Batch-1 layers as three kernels each: [LN1 + QKV (+ clear the MLP's accumulator)] ->
-        [attention + out-projection, 4 head-group slabs] -> [add + LN2 + c_fc + GELU + c_proj, added
-        into the int64 fixed-point residual xr[l % 2]].  Layer 0 reads the f32 embedding row x; the
-        final residual is xr[(L - 1) % 2]."""
+        """Layers as [LN1 + QKV (+ clear the MLP's accumulator)] -> attention + out-projection ->
+        [add + LN2 + c_fc + GELU + c_proj, added into the int64 fixed-point residual xr[l % 2]].
+        Batch 1: attention fused with the out-projection (4 head-group slabs the MLP sums); 2 or more
+        rows: split attention, then the skinny out-projection adding into the residual in place (the
+        f32 embedding rows x in layer 0, copy 0 of the fixed-point residual after that).  The final
+        residual is xr[(L - 1) % 2]."""
         eps = self.cfg.layer_norm_epsilon
         xin = self.x[:B]
         for li, lw in enumerate(self.w.layers):
             kc, vc = self.kv[li, 0], self.kv[li, 1]
             acc = self.xr[li % 2, :, :B]
             ops.skinny_addln_gemm(xin, lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, bias=lw.b_qkv, q_out=r.q,
-                                  k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos, zero=acc)
-            ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
-                                        self.ao_groups, tiles=self.ao_group_tiles)
-            ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc,
-                           parts=self.ao_parts[:4, :1], nsplit=4, res_bias=lw.b_o)
+                                  k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos,
+                                  zero=self.xr[li % 2])  # (all of its rows: a contiguous clear)
+            if B == 1:
+                ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
+                                            self.ao_groups, tiles=self.ao_group_tiles)
+                ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc,
+                               parts=self.ao_parts[:4, :1], nsplit=4, res_bias=lw.b_o)
+            else:
+                self._attn(r, li)
+                ops.skinny_gemm(self.att[:B], lw.w_o_sh, ops.EPI_F32, bias=lw.b_o, out=xin if li == 0 else xin[0])
+                ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc)
             xin = acc
 
     def _small_overlap_ok(self, B: int) -> bool:

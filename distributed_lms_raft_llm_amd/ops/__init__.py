@@ -723,7 +723,8 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
     ``ln=(gamma, beta, eps)``: ``a`` is the f32 residual x [M, K] and the kernel LayerNorms it in
     its prologue (EPI_BF16 / EPI_GELU_TANH / EPI_QKV / EPI_ARGMAX: ln_f fused into the LM head);
     otherwise ``a`` is bf16 [M, K].
-    EPI_F32 adds ``acc + bias`` into ``out`` (f32 [M, N], in place: the residual stream);
+    EPI_F32 adds ``acc + bias`` into ``out`` (f32 [M, N], in place: the residual stream; an int64
+    ``out`` is copy 0 of ``skinny_mlp``'s fixed-point residual and gets fix(acc + bias) added);
     EPI_PARTIAL stores the raw f32 partial (TP); EPI_ARGMAX writes one key per (row, 64 columns)
     into ``argmax_out`` [M, >= N/64] exactly like ``gemm(..., EPI_ARGMAX)``."""
     _req(w_sh, torch.bfloat16, "w_sh", 4)
@@ -757,8 +758,13 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
         if bias.numel() < N:
             raise ValueError("bias too short")
         ep.bias = bias.data_ptr()
+    cepi = epi
+    if epi == EPI_F32 and out is not None and out.dtype == torch.int64:
+        cepi = 7  # skinny.hip SK_FIXADD: into copy 0 of the fused MLP's fixed-point residual
     if epi in (EPI_BF16, EPI_GELU_TANH, EPI_F32, EPI_PARTIAL):
         want = torch.bfloat16 if epi in (EPI_BF16, EPI_GELU_TANH) else torch.float32
+        if cepi == 7:
+            want = torch.int64
         if out is None:
             if epi == EPI_F32:
                 raise ValueError("skinny_gemm EPI_F32 accumulates into an existing out (the residual)")
@@ -797,7 +803,7 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
     else:
         raise ValueError(f"skinny_gemm: unsupported epilogue {epi}")
     lg, lb, le = (ln[0], ln[1], float(ln[2])) if ln is not None else (None, None, 0.0)
-    _check(lib().dlms_skinny_gemm(epi, _p(a), a.stride(0), _p(lg), _p(lb), le, _p(w_sh), M, N, K, ctypes.byref(ep),
+    _check(lib().dlms_skinny_gemm(cepi, _p(a), a.stride(0), _p(lg), _p(lb), le, _p(w_sh), M, N, K, ctypes.byref(ep),
                                   _stream()), "dlms_skinny_gemm")
     return out
 

@@ -23,7 +23,9 @@
 #include <type_traits>
 #include <stdlib.h>
 
-enum { SK_BF16 = 0, SK_GELU_TANH = 1, SK_F32 = 3, SK_QKV = 4, SK_ARGMAX = 5, SK_PARTIAL = 6 };
+// SK_FIXADD: like SK_F32 (x += acc + bias, column-owning, in place) into copy 0 of the int64
+// fixed-point residual the fused MLP accumulates (see DLMS_FIX_SCALE below)
+enum { SK_BF16 = 0, SK_GELU_TANH = 1, SK_F32 = 3, SK_QKV = 4, SK_ARGMAX = 5, SK_PARTIAL = 6, SK_FIXADD = 7 };
 
 #define SK_MAX_LN_V4 8  // LN prologue: K <= 64 lanes * 4 * 8 = 2048
 
@@ -127,6 +129,9 @@ __device__ __forceinline__ void skinny_store(const f32x4_t* acc, int M, int col,
             } else if constexpr (EPI == SK_F32) {
                 float* o = reinterpret_cast<float*>(ep.out) + (size_t)row * ep.ldo + col;
                 *o = *o + v;  // residual stream, updated in place (x is not an operand of this GEMM)
+            } else if constexpr (EPI == SK_FIXADD) {
+                long long* o = reinterpret_cast<long long*>(ep.out) + (size_t)row * ep.ldo + col;
+                *o = *o + __float2ll_rn(v * 4294967296.0f);  // DLMS_FIX_SCALE (defined further down)
             } else if constexpr (EPI == SK_PARTIAL) {
                 reinterpret_cast<float*>(ep.out)[(size_t)row * ep.ldo + col] = acc[t][r];
             } else if constexpr (EPI == SK_QKV) {
@@ -310,7 +315,7 @@ static hipError_t skinny_dispatch(const void* A, int lda, const float* g, const 
                                   int M, int N, int K, const GemmEpi& ep, hipStream_t stream) {
     if constexpr (EPI == SK_ARGMAX) {
         return skinny_kbw<EPI, LN, MT, 16, 4>(A, lda, g, b, eps, W, M, N, K, ep, stream);
-    } else if constexpr (EPI == SK_F32 || EPI == SK_PARTIAL) {
+    } else if constexpr (EPI == SK_F32 || EPI == SK_FIXADD || EPI == SK_PARTIAL) {
         if (K > 2048) return skinny_kbw<EPI, LN, MT, 16, 1>(A, lda, g, b, eps, W, M, N, K, ep, stream);
         return skinny_kbw<EPI, LN, MT, 8, 1>(A, lda, g, b, eps, W, M, N, K, ep, stream);
     } else {
@@ -347,6 +352,7 @@ extern "C" hipError_t dlms_skinny_gemm(int epi, const void* A, int lda, const fl
         SK_LN(SK_GELU_TANH)
         SK_LN(SK_QKV)
         SK_NOLN(SK_F32)
+        SK_NOLN(SK_FIXADD)
         case SK_ARGMAX:  // with the LN prologue: ln_f fused into the latency path's LM head
             return ln ? skinny_mt<SK_ARGMAX, true>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream)
                       : skinny_mt<SK_ARGMAX, false>(A, lda, ln_g, ln_b, eps, W, M, N, K, *ep, stream);

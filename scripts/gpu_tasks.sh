@@ -23,6 +23,7 @@
 #   e2e1:<n>         the same with the tutor at TP=1 (one-GPU boxes: configs 4/5 ask for TP=4/8)
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
 #   sweep1:<...>     the same at batch 1 and 2 (p50 per query)     -> gpurun_out/sweep1.jsonl
+#   sweep4:<...>     the same at batch 3 and 4
 #   sweep32:<...>    the same at batch 16 and 32                   -> gpurun_out/sweep1.jsonl
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -109,9 +110,9 @@ for task in "$@"; do
                 echo "{\"env\": \"$envs\", \"bench\": $(grep '^{' gpurun_out/sweep.log | tail -1)}" >> gpurun_out/sweep.jsonl
                 tail -1 gpurun_out/sweep.jsonl
             done ;;
-        sweep1:*|sweep32:*)  # the same at batch 1 and 2 / 16 and 32: value = tok/s, plus p50 per query
+        sweep1:*|sweep4:*|sweep32:*)  # the same at batch 1 and 2 / 3 and 4 / 16 and 32: p50 per query
             IFS=';' read -ra sets <<< "${task#*:}"
-            bs="1 2"; [[ $task == sweep32:* ]] && bs="16 32"
+            bs="1 2"; [[ $task == sweep32:* ]] && bs="16 32"; [[ $task == sweep4:* ]] && bs="3 4"
             for envs in "${sets[@]}"; do
                 for b in $bs; do
                     step 300 gpurun_out/sweep1.log env ${envs//,/ } python -u bench.py --batch $b --steps 8 --warmup 2 --latency-batches ""

@@ -117,6 +117,24 @@ def test_fused_mlp_batch1(name, monkeypatch):
     _assert_teacher_forced(GPT2Reference(cfg, w, device="cuda"), plain.generate(prompts), prompts)
 
 
+@pytest.mark.parametrize("batch,rows", [(2, "2"), (3, "4")])
+def test_fused_mlp_small_batch(batch, rows, monkeypatch):
+    """2+ rows on the fused-MLP path (split attention, out-projection added in place into the
+    fixed-point residual): exact under the margin rule, identical across graph / eager and runs."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+    from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference
+
+    monkeypatch.setenv("DLMS_FUSED_MLP_ROWS", rows)
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [13, 4, 27][:batch], seed=23)
+    eng = HipGPT2Engine(cfg, w, max_batch=8, max_length=64)
+    assert eng.fused_mlp_rows >= batch
+    a = eng.generate(prompts)
+    assert eng.generate(prompts) == a
+    assert HipGPT2Engine(cfg, w, max_batch=8, max_length=64, use_graph=False).generate(prompts) == a
+    _assert_teacher_forced(GPT2Reference(cfg, w, device="cuda"), a, prompts)
+
+
 def test_graph_replay_equals_eager():
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 

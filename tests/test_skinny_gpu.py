@@ -443,6 +443,21 @@ def test_skinny_addln_qkv_fixed_point_and_zero(M):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("M", [1, 2, 5])
+def test_skinny_fixed_point_residual_add(M):
+    """EPI_F32 into an int64 residual: copy 0 += fix(a W^T + b), column-owning and in place."""
+    ops = _ops()
+    N, K = 768, 768
+    a = _rand(M, K, seed=241)
+    w = _rand(N, K, scale=0.05, seed=242)
+    bias = _rand(N, seed=243, dtype=torch.float32)
+    x = _rand(M, N, seed=244, dtype=torch.float32)
+    xf = _to_fix(x)
+    ops.skinny_gemm(a, ops.shuffle_weight(w), ops.EPI_F32, bias=bias, out=xf[0])
+    ref = x + a.float() @ w.float().t() + bias
+    torch.testing.assert_close(ops.fix_to_float(xf), ref, atol=2e-3, rtol=1e-3)
+
+
 @pytest.mark.parametrize("M,K", [(1, 768), (3, 1024), (2, 1600)])
 def test_ln_fix(M, K):
     ops = _ops()
