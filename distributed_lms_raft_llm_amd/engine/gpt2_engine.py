@@ -212,6 +212,10 @@ class HipGPT2Engine:
         # profiles/r1_split_cap_insitu.log; DLMS_OVERLAP_SPLIT_CAP overrides.
         self.overlap_split_cap = int(os.environ.get("DLMS_OVERLAP_SPLIT_CAP", "2"))
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
+        # decode steps per graph replay in the overlapped step: the row parts run that many steps each
+        # on their own stream before joining (rows are independent sequences), so a part that gets
+        # ahead is not held back at every step's join
+        self.steps_per_graph = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH", "1")))
         # overlapped step's attention: persistent grid of this many 4-wave workgroups (0 = one wave
         # per (row, head) pair, the default: 256/512/1024 blocks measured -6 % / +0.3 % / +1 %, i.e.
         # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
@@ -562,7 +566,7 @@ class HipGPT2Engine:
         else:
             self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
 
-    def _decode_step_overlap(self, B: int, penalty: float):
+    def _decode_step_overlap(self, B: int, penalty: float, nsteps: int = 1):
         """Decode step as ``overlap_parts`` row ranges on as many HIP streams (one hardware queue
         each), free-running: the decode GEMMs are latency-bound (a near-constant ~12 us per launch
         whatever M, profiles/r1_gemm_lab) and attention is HBM-bound, so independent row ranges
@@ -583,13 +587,16 @@ class HipGPT2Engine:
         step = B // k
         parts = [(i * step, self._part_rows(i * step, (i + 1) * step)) for i in range(k)]
         if k == 2 and os.environ.get("DLMS_OVERLAP_SERIAL", "0") == "1":
-            self._two_halves_serialised(parts, streams, penalty)
+            for _ in range(nsteps):
+                self._two_halves_serialised(parts, streams, penalty)
         elif self.alt_attn:
-            self._alternating_attention(parts, streams, penalty)
+            for _ in range(nsteps):
+                self._alternating_attention(parts, streams, penalty)
         else:
             for (lo, r), s in zip(parts, streams):
                 with torch.cuda.stream(s):
-                    self._part_step(r, lo, penalty)
+                    for _ in range(nsteps):
+                        self._part_step(r, lo, penalty)
         for s in streams[1:]:
             cur.wait_stream(s)
 
@@ -786,7 +793,13 @@ class HipGPT2Engine:
         for s in streams[1:]:
             cur.wait_stream(s)
 
-    def _decode_step(self, B: int, penalty: float):
+    def _decode_step(self, B: int, penalty: float, nsteps: int = 1):
+        if nsteps > 1:
+            if self._overlap_ok(B) and not self._small_ok(B) and not self._small_overlap_ok(B):
+                return self._decode_step_overlap(B, penalty, nsteps)
+            for _ in range(nsteps):
+                self._decode_step(B, penalty)
+            return
         if self._small_ok(B):
             return self._decode_step_small(B, penalty)
         if self._small_overlap_ok(B):
@@ -800,8 +813,8 @@ class HipGPT2Engine:
         else:
             self._lm_head_and_update(self.h[:B], B, penalty)
 
-    def _graph_for(self, B: int, penalty: float) -> torch.cuda.CUDAGraph:
-        key = (B, float(penalty))
+    def _graph_for(self, B: int, penalty: float, nsteps: int = 1) -> torch.cuda.CUDAGraph:
+        key = (B, float(penalty), nsteps)
         g = self._graphs.get(key)
         if g is None:
             # warm up on a side stream (kernel code objects loaded, RCCL comm initialised)
@@ -809,14 +822,14 @@ class HipGPT2Engine:
             s.wait_stream(torch.cuda.current_stream())
             saved = self._snapshot_state(B)
             with torch.cuda.stream(s):
-                self._decode_step(B, penalty)
+                self._decode_step(B, penalty, nsteps)
             torch.cuda.current_stream().wait_stream(s)
             self._restore_state(B, saved)
             # (one graph per row part replayed on its own stream measured identical to this one
             # forked graph: 668.07 vs 668.08 k tok/s, profiles/r2_sweep_split_graphs.jsonl)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._decode_step(B, penalty)
+                self._decode_step(B, penalty, nsteps)
             self._restore_state(B, saved)
             self._graphs[key] = g
         return g
@@ -1095,6 +1108,9 @@ class HipGPT2Engine:
         ev1.record()
         steps_max = T - min(len(p) for p in prompts) - 1
         graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
+        kg = self.steps_per_graph if (graph is not None and self._overlap_ok(B) and not self._small_ok(B) and
+                                      self.check_every % self.steps_per_graph == 0) else 1
+        graph_k = self._graph_for(B, repetition_penalty, kg) if kg > 1 and steps_max >= kg else None
         steps = 0
         # Stop check one chunk behind: the all-finished flag of chunk k is copied to pinned host
         # memory asynchronously and read after chunk k+1 has been enqueued, so the GPU never idles
@@ -1103,7 +1119,12 @@ class HipGPT2Engine:
         pending = None
         while steps < steps_max:
             chunk = min(self.check_every, steps_max - steps)
-            for _ in range(chunk):
+            done_k = 0
+            if graph_k is not None:
+                for _ in range(chunk // kg):
+                    graph_k.replay()
+                done_k = chunk // kg * kg
+            for _ in range(chunk - done_k):
                 if graph is not None:
                     graph.replay()
                 else:

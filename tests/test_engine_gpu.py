@@ -221,6 +221,21 @@ def test_overlapped_multi_stream_step_equals_serial(use_graph, parts, serial, mo
     assert a == b
 
 
+def test_multi_step_graph_equals_single_step(monkeypatch):
+    """Several decode steps per graph replay (each row part runs them back to back on its own
+    stream, joining once per replay) compute exactly what one step per replay computes."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [32] * 6 + [9, 17, 3, 25], seed=5)
+    kw = dict(max_batch=16, max_length=72, overlap=True, overlap_min_batch=2, overlap_parts=2)
+    a = HipGPT2Engine(cfg, w, **kw).generate(prompts)
+    monkeypatch.setenv("DLMS_STEPS_PER_GRAPH", "4")
+    eng = HipGPT2Engine(cfg, w, **kw)
+    assert eng.steps_per_graph == 4
+    assert eng.generate(prompts) == a
+
+
 def test_overlap_split_cap_tracks_serial():
     """With the production split-K cap for concurrent row parts only the fp32 summation order of
     the row-parallel partials changes: the greedy tokens track the single-stream step."""
