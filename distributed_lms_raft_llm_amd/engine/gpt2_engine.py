@@ -595,8 +595,10 @@ class HipGPT2Engine:
         else:
             for (lo, r), s in zip(parts, streams):
                 with torch.cuda.stream(s):
-                    for _ in range(nsteps):
-                        self._part_step(r, lo, penalty)
+                    for i in range(nsteps):
+                        # (fresh row state per step: _Rows carries the residual update pending
+                        # between layers, which the last layer of a step leaves set)
+                        self._part_step(r if i == 0 else self._part_rows(lo, lo + step), lo, penalty)
         for s in streams[1:]:
             cur.wait_stream(s)
 
