@@ -214,8 +214,9 @@ class HipGPT2Engine:
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
         # decode steps per graph replay in the overlapped step: the row parts run that many steps each
         # on their own stream before joining (rows are independent sequences), so a part that gets
-        # ahead is not held back at every step's join
-        self.steps_per_graph = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH", "1")))
+        # ahead is not held back at every step's join.  1024 queries, one box: 1 step 683 / 682 k
+        # tok/s, 2 steps 697 k, 4 steps 698 / 696 k, 16 steps 698 k (profiles/r2_sweep_steps_per_graph.jsonl)
+        self.steps_per_graph = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH", "4")))
         # overlapped step's attention: persistent grid of this many 4-wave workgroups (0 = one wave
         # per (row, head) pair, the default: 256/512/1024 blocks measured -6 % / +0.3 % / +1 %, i.e.
         # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
