@@ -587,12 +587,15 @@ class HipGPT2Engine:
             s.wait_stream(cur)
         step = B // k
         parts = [(i * step, self._part_rows(i * step, (i + 1) * step)) for i in range(k)]
+        def fresh(i):  # per-step row state (the pending residual update must not carry across steps)
+            return parts if i == 0 else [(lo, self._part_rows(lo, lo + step)) for lo, _ in parts]
+
         if k == 2 and os.environ.get("DLMS_OVERLAP_SERIAL", "0") == "1":
-            for _ in range(nsteps):
-                self._two_halves_serialised(parts, streams, penalty)
+            for i in range(nsteps):
+                self._two_halves_serialised(fresh(i), streams, penalty)
         elif self.alt_attn:
-            for _ in range(nsteps):
-                self._alternating_attention(parts, streams, penalty)
+            for i in range(nsteps):
+                self._alternating_attention(fresh(i), streams, penalty)
         else:
             for (lo, r), s in zip(parts, streams):
                 with torch.cuda.stream(s):
