@@ -217,6 +217,10 @@ class HipGPT2Engine:
         # ahead is not held back at every step's join.  1024 queries, one box: 1 step 683 / 682 k
         # tok/s, 2 steps 697 k, 4 steps 698 / 696 k, 16 steps 698 k (profiles/r2_sweep_steps_per_graph.jsonl)
         self.steps_per_graph = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH", "4")))
+        # the same for every other decode step shape (latency path, tiled single-stream step): one
+        # replay per this many steps (fewer graph launches between dependent steps): batch 1
+        # 32.6-32.8 -> 32.2 ms, batch 2 35.0 -> 34.5, batch 32 57.3 -> 55.5 (r2_sweep_steps_per_graph.jsonl)
+        self.steps_per_graph_small = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH_SMALL", "4")))
         # overlapped step's attention: persistent grid of this many 4-wave workgroups (0 = one wave
         # per (row, head) pair, the default: 256/512/1024 blocks measured -6 % / +0.3 % / +1 %, i.e.
         # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
@@ -1114,8 +1118,10 @@ class HipGPT2Engine:
         ev1.record()
         steps_max = T - min(len(p) for p in prompts) - 1
         graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
-        kg = self.steps_per_graph if (graph is not None and self._overlap_ok(B) and not self._small_ok(B) and
-                                      self.check_every % self.steps_per_graph == 0) else 1
+        overlapped = self._overlap_ok(B) and not self._small_ok(B) and not self._small_overlap_ok(B)
+        kg = self.steps_per_graph if overlapped else self.steps_per_graph_small
+        if graph is None or self.check_every % kg:
+            kg = 1
         graph_k = self._graph_for(B, repetition_penalty, kg) if kg > 1 and steps_max >= kg else None
         steps = 0
         # Stop check one chunk behind: the all-finished flag of chunk k is copied to pinned host

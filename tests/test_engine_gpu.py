@@ -236,6 +236,22 @@ def test_multi_step_graph_equals_single_step(monkeypatch):
     assert eng.generate(prompts) == a
 
 
+@pytest.mark.parametrize("batch", [1, 2, 5, 24])
+def test_multi_step_graph_small_paths(batch, monkeypatch):
+    """Latency path (fused MLP at 1-2 rows, 4-kernel step at 5) and the tiled step (24 rows) with
+    4 steps per graph replay: the same tokens as one step per replay."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [5 + (7 * i) % 27 for i in range(batch)], seed=29)
+    monkeypatch.setenv("DLMS_STEPS_PER_GRAPH_SMALL", "1")
+    a = HipGPT2Engine(cfg, w, max_batch=max(8, batch), max_length=61).generate(prompts)
+    monkeypatch.setenv("DLMS_STEPS_PER_GRAPH_SMALL", "4")
+    eng = HipGPT2Engine(cfg, w, max_batch=max(8, batch), max_length=61)
+    assert eng.steps_per_graph_small == 4
+    assert eng.generate(prompts) == a
+
+
 def test_overlap_split_cap_tracks_serial():
     """With the production split-K cap for concurrent row parts only the fp32 summation order of
     the row-parallel partials changes: the greedy tokens track the single-stream step."""
