@@ -1039,11 +1039,22 @@ class HipGPT2Engine:
         if B > self.max_batch or B not in (_bucket(B), self.max_batch):
             raise ValueError(f"decode: batch bucket {B} invalid")
         graph = self._graph_for(B, repetition_penalty) if self.use_graph else None
-        for _ in range(steps):
+        kg = self._steps_per_graph_for(B) if graph is not None else 1
+        n_k = steps // kg if kg > 1 else 0
+        if n_k:
+            graph_k = self._graph_for(B, repetition_penalty, kg)
+            for _ in range(n_k):
+                graph_k.replay()
+        for _ in range(steps - n_k * kg):
             if graph is not None:
                 graph.replay()
             else:
                 self._decode_step(B, repetition_penalty)
+
+    def _steps_per_graph_for(self, B: int) -> int:
+        """Decode steps per graph replay for a batch bucket (DLMS_STEPS_PER_GRAPH[_SMALL])."""
+        overlapped = self._overlap_ok(B) and not self._small_ok(B) and not self._small_overlap_ok(B)
+        return self.steps_per_graph if overlapped else self.steps_per_graph_small
 
     def health_async(self) -> "HostResult | None":
         """Non-zero ``.result()`` when a TP collective gave up waiting for a peer (the xGMI
@@ -1118,8 +1129,7 @@ class HipGPT2Engine:
         ev1.record()
         steps_max = T - min(len(p) for p in prompts) - 1
         graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
-        overlapped = self._overlap_ok(B) and not self._small_ok(B) and not self._small_overlap_ok(B)
-        kg = self.steps_per_graph if overlapped else self.steps_per_graph_small
+        kg = self._steps_per_graph_for(B)
         if graph is None or self.check_every % kg:
             kg = 1
         graph_k = self._graph_for(B, repetition_penalty, kg) if kg > 1 and steps_max >= kg else None
