@@ -299,7 +299,10 @@ class HipGPT2Engine:
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
         self.lm_head_sh = None
-        ps_lm = self.max_batch >= self.PS_LM_MIN_ROWS and os.environ.get("DLMS_PS_LMHEAD", "1") != "0"
+        # (gemm_ps streams K in 128-deep register chunks: GPT-2-XL's K = 1600 keeps the tiled LM head)
+        ps_lm = (self.max_batch >= self.PS_LM_MIN_ROWS and cfg.n_embd % 128 == 0 and
+                 os.environ.get("DLMS_PS_LMHEAD", "1") != "0")
+        self.ps_lm = ps_lm and not self.w.fp8
         if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
             # (the latency path's skinny LM head reads the same pre-shuffled copy)
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
@@ -515,9 +518,8 @@ class HipGPT2Engine:
         P = self.key_parts.shape[1]  # partial keys per row the LM head writes (and the consumer reads)
         if keys_ready:  # the caller ran the LM head (skinny, ln_f fused): one key per 64 columns
             P = self.lm_head_sh.shape[0] * 16 // 64
-        elif hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B >= self.PS_LM_MIN_ROWS and \
-                self.max_batch >= self.PS_LM_MIN_ROWS:
-            P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16)
+        elif hidden.dtype != ops.FP8 and self.ps_lm and B >= self.PS_LM_MIN_ROWS:
+            P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16, self.lm_head_sh.shape[1] * 32)
             ops.gemm_ps(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                         vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
         elif hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B <= self.small_max and self.lm_skinny:

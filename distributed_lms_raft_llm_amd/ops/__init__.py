@@ -1188,11 +1188,17 @@ def attention_oproj_grouped(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
 PS_WAVES = 8
 
 
-def gemm_ps_geometry(M: int, N: int, epi: int, split: int = 1, cus: int = 256):
+PS_LDS_BYTES = 160 * 1024  # gemm_ps.hip: activation panel (16 mt rows of kc * 2 + 32 B) + 8 x 4 KiB staging
+
+
+def gemm_ps_geometry(M: int, N: int, epi: int, split: int = 1, cus: int = 256, K: int = 768):
     """(mt, nt, col_wgs) for ``gemm_ps``: 64-row blocks when the LM head's weight reuse matters
-    (and the panel fits), else 32; column workgroups sized so the grid covers the CUs about once
-    (the LM head loops over its tiles inside each wave)."""
-    mt = 4 if (epi == EPI_ARGMAX or M >= 512) else 2
+    and the K / split panel fits in LDS (K <= 1008: GPT-2-small; the wider models take 32-row
+    blocks), else 32; column workgroups sized so the grid covers the CUs about once (the LM head
+    loops over its tiles inside each wave)."""
+    kc = K // max(1, split)
+    fits4 = 64 * (kc * 2 + 32) + 8 * 4096 <= PS_LDS_BYTES
+    mt = 4 if ((epi == EPI_ARGMAX or M >= 512) and fits4) else 2
     nt = 2
     row_blocks = -(-M // (16 * mt))
     tiles = N // (16 * nt)
@@ -1220,7 +1226,7 @@ def gemm_ps(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, bias=None, out=Non
         raise ValueError("gemm_ps: K / split_k must be a multiple of 128")
     if epi != EPI_PARTIAL and split_k != 1:
         raise ValueError("gemm_ps: split_k only with EPI_PARTIAL")
-    mt, nt, col_wgs = geometry or gemm_ps_geometry(M, N, epi, split_k)
+    mt, nt, col_wgs = geometry or gemm_ps_geometry(M, N, epi, split_k, K=K)
     if N % (16 * nt):
         raise ValueError("gemm_ps: N must be a multiple of 16 * nt")
     ep = GemmEpi()
@@ -1280,6 +1286,6 @@ def gemm_ps(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, bias=None, out=Non
     return out
 
 
-def gemm_ps_key_slots(M: int, N: int) -> int:
-    """argmax_out columns ``gemm_ps(..., EPI_ARGMAX)`` writes for an M x N LM head."""
-    return PS_WAVES * gemm_ps_geometry(M, N, EPI_ARGMAX)[2]
+def gemm_ps_key_slots(M: int, N: int, K: int = 768) -> int:
+    """argmax_out columns ``gemm_ps(..., EPI_ARGMAX)`` writes for an M x N x K LM head."""
+    return PS_WAVES * gemm_ps_geometry(M, N, EPI_ARGMAX, K=K)[2]

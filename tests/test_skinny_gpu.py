@@ -518,19 +518,20 @@ def test_gemm_ps_qkv(M):
     torch.testing.assert_close(vs, z[:, 2 * D:], atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [3, 64, 512])
-def test_gemm_ps_argmax_matches_tiled(M):
+@pytest.mark.parametrize("M,K", [(3, 768), (64, 768), (512, 768), (512, 1024), (1024, 1024), (256, 1280)])
+def test_gemm_ps_argmax_matches_tiled(M, K):
     """Same keys as the tiled LM head's fused penalty + argmax (identical per-element sums are not
-    required: compare the decoded token wherever the fp32 top-2 margin is clear)."""
+    required: compare the decoded token wherever the fp32 top-2 margin is clear); K > 1008 (GPT-2
+    medium and wider) takes 32-row panels so the panel fits in LDS."""
     ops = _ops()
-    V, K = 50257, 768
+    V = 50257
     Vp = 50304
     h = _rand(M, K, seed=131)
     w = _rand(Vp, K, scale=0.05, seed=132)
     seen = torch.randint(-2**31, 2**31 - 1, (M, Vp // 32), generator=torch.Generator().manual_seed(3),
                          dtype=torch.int64).to(torch.int32).to(DEV)
     seen &= 0x01010101  # ~1/8 of the vocabulary penalised
-    keys = torch.zeros(M, ops.gemm_ps_key_slots(M, Vp), dtype=torch.int64, device=DEV)
+    keys = torch.zeros(M, ops.gemm_ps_key_slots(M, Vp, K), dtype=torch.int64, device=DEV)
     ops.gemm_ps(h, ops.shuffle_weight(w), ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2)
     tok = ops.argmax_reduce(keys)
     got = ((~(tok & 0xFFFFFFFF)) & 0xFFFFFFFF).cpu()
