@@ -299,8 +299,11 @@ class HipGPT2Engine:
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
         self.lm_head_sh = None
-        # (gemm_ps streams K in 128-deep register chunks: GPT-2-XL's K = 1600 keeps the tiled LM head)
+        # (only where its 64-row panel fits in LDS, i.e. GPT-2-small: with 32-row panels GPT-2-medium
+        # ran 254.8 k tok/s against 279.9 k on the tiled LM head; XL's K = 1600 is not a multiple of
+        # its 128-deep register chunks either)
         ps_lm = (self.max_batch >= self.PS_LM_MIN_ROWS and cfg.n_embd % 128 == 0 and
+                 64 * (2 * cfg.n_embd + 32) + 8 * 4096 <= ops.PS_LDS_BYTES and
                  os.environ.get("DLMS_PS_LMHEAD", "1") != "0")
         self.ps_lm = ps_lm and not self.w.fp8
         if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
