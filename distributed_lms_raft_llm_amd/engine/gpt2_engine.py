@@ -242,8 +242,12 @@ class HipGPT2Engine:
         if latency_path is None:
             latency_path = os.environ.get("DLMS_LATENCY_PATH", "1") != "0"
         self.small_max = ops.skinny_addln_max_rows(cfg.n_embd) if (latency_path and not self.w.fp8) else 0
-        if self.tp_size == 1 and any((k // 64) % self.SMALL_SPLIT for k in (self.w.d_local, self.w.ffn_local)):
-            self.small_max = 0  # the fused add+LN kernel sums exactly SMALL_SPLIT slabs (tiny test models)
+        inplace_ok = self.tp_size == 1 and os.environ.get("DLMS_SMALL_INPLACE", "1") != "0"
+        if self.tp_size == 1 and not inplace_ok and \
+                any((k // 64) % self.SMALL_SPLIT for k in (self.w.d_local, self.w.ffn_local)):
+            # the fused add+LN kernel sums exactly SMALL_SPLIT slabs (tiny test models; GPT-2-XL's 25
+            # heads) -- only without the in-place projections, which leave no slabs to sum
+            self.small_max = 0
         if self.small_max:
             for lw in self.w.layers:  # MFMA-fragment-order copies of the QKV / c_fc weights
                 if lw.w_qkv_sh is None:

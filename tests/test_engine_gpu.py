@@ -62,7 +62,7 @@ def _assert_teacher_forced(model, outs, prompts, eps=0.05, min_decisive=0.7):
 
 
 @pytest.mark.parametrize("name,batch", [("gpt2-tiny", 3), ("gpt2", 1), ("gpt2", 3), ("gpt2", 8), ("gpt2", 24),
-                                        ("gpt2-medium", 1), ("gpt2-medium", 2)])
+                                        ("gpt2-medium", 1), ("gpt2-medium", 2), ("gpt2-xl", 2)])
 def test_generate_matches_reference_tokens(name, batch):
     """bf16 engine vs fp32 oracle, margin-aware and exact: batch 3/8 run the latency path
     (fused add+LN skinny GEMMs, split-K attention), 24 the tiled path."""
