@@ -222,9 +222,10 @@ class HipGPT2Engine:
         # 32.6-32.8 -> 32.2 ms, batch 2 35.0 -> 34.5, batch 32 57.3 -> 55.5 (r2_sweep_steps_per_graph.jsonl)
         self.steps_per_graph_small = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH_SMALL", "4")))
         # overlapped step's attention: persistent grid of this many 4-wave workgroups (0 = one wave
-        # per (row, head) pair, the default: 256/512/1024 blocks measured -6 % / +0.3 % / +1 %, i.e.
-        # noise, at 1024 queries -- profiles/r2_sweep_persist.jsonl); DLMS_PERSIST_ATTN_BLOCKS overrides
-        self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "0"))
+        # per (row, head) pair).  With one join per step it measured noise (profiles/r2_sweep_persist.jsonl);
+        # with the row parts running 4 steps between joins, 512 blocks leave the other part's GEMMs
+        # wave slots: 682.7 / 684.5 -> 691.5 / 691.1 k tok/s on one box (r2_sweep_persist_multistep.jsonl)
+        self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "512"))
         self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
         # latency path, TP=1: ln_f fused into a skinny LM head (one kernel fewer per token) -- opt-in:
         # the skinny LM head is slower than the tiled one by more than the launch it saves
