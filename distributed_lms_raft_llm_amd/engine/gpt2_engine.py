@@ -215,8 +215,9 @@ class HipGPT2Engine:
         # decode steps per graph replay in the overlapped step: the row parts run that many steps each
         # on their own stream before joining (rows are independent sequences), so a part that gets
         # ahead is not held back at every step's join.  1024 queries, one box: 1 step 683 / 682 k
-        # tok/s, 2 steps 697 k, 4 steps 698 / 696 k, 16 steps 698 k (profiles/r2_sweep_steps_per_graph.jsonl)
-        self.steps_per_graph = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH", "4")))
+        # tok/s, 2 steps 697 k, 4 steps 698 / 696 k, 16 steps 698 k (profiles/r2_sweep_steps_per_graph.jsonl);
+        # with the 768-block persistent attention 8 steps: decode 156.9 vs 157.9 ms at 4
+        self.steps_per_graph = max(1, int(os.environ.get("DLMS_STEPS_PER_GRAPH", "8")))
         # the same for every other decode step shape (latency path, tiled single-stream step): one
         # replay per this many steps (fewer graph launches between dependent steps): batch 1
         # 32.6-32.8 -> 32.2 ms, batch 2 35.0 -> 34.5, batch 32 57.3 -> 55.5 (r2_sweep_steps_per_graph.jsonl)
@@ -224,8 +225,9 @@ class HipGPT2Engine:
         # overlapped step's attention: persistent grid of this many 4-wave workgroups (0 = one wave
         # per (row, head) pair).  With one join per step it measured noise (profiles/r2_sweep_persist.jsonl);
         # with the row parts running 4 steps between joins, 512 blocks leave the other part's GEMMs
-        # wave slots: 682.7 / 684.5 -> 691.5 / 691.1 k tok/s on one box (r2_sweep_persist_multistep.jsonl)
-        self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "512"))
+        # wave slots: 682.7 / 684.5 -> 691.5 / 691.1 k tok/s on one box; decode ms per generation over
+        # three boxes: 256 blocks 169.2, 512 158.8, 768 157.9, 1024 160.1 (r2_sweep_persist_multistep.jsonl)
+        self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "768"))
         self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
         # latency path, TP=1: ln_f fused into a skinny LM head (one kernel fewer per token) -- opt-in:
         # the skinny LM head is slower than the tiled one by more than the launch it saves
