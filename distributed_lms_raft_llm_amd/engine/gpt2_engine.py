@@ -316,6 +316,11 @@ class HipGPT2Engine:
         if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
             # (the latency path's skinny LM head reads the same pre-shuffled copy)
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
+        # batch 1-2 (TP=1, bf16): the persistent dataflow decode -- one launch per chunk of decode
+        # steps (ops/dataflow.py); built on first use (it packs a per-CU copy of the weights)
+        self.dataflow = (os.environ.get("DLMS_DATAFLOW", "0") != "0" and tp_group is None and
+                         not self.w.fp8 and self._df_supported())
+        self._df = None
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -671,6 +676,23 @@ class HipGPT2Engine:
                     last_gemm.record(s)
                     if p < L:
                         self._attn(r, p)
+
+    def _df_supported(self) -> bool:
+        from ..ops.dataflow import DataflowDecoder
+
+        return DataflowDecoder.supported(self)
+
+    def _df_ok(self, B: int) -> bool:
+        from ..ops.dataflow import MAX_ROWS
+
+        return self.dataflow and 1 <= B <= min(MAX_ROWS, self.max_batch)
+
+    def _df_decoder(self):
+        if self._df is None:
+            from ..ops.dataflow import DataflowDecoder
+
+            self._df = DataflowDecoder(self)
+        return self._df
 
     def _small_ok(self, B: int) -> bool:
         return 0 < B <= self.small_max
@@ -1050,6 +1072,9 @@ class HipGPT2Engine:
         """``steps`` greedy decode steps over slots [0, B) (finished/inert slots are no-ops)."""
         if B > self.max_batch or B not in (_bucket(B), self.max_batch):
             raise ValueError(f"decode: batch bucket {B} invalid")
+        if steps > 0 and self._df_ok(B):
+            self._df_decoder().run(B, steps, repetition_penalty)
+            return
         graph = self._graph_for(B, repetition_penalty) if self.use_graph else None
         kg = self._steps_per_graph_for(B) if graph is not None else 1
         n_k = steps // kg if kg > 1 else 0
@@ -1140,6 +1165,25 @@ class HipGPT2Engine:
         self._prefill(prompts, B, repetition_penalty)
         ev1.record()
         steps_max = T - min(len(p) for p in prompts) - 1
+        if steps_max > 0 and self._df_ok(B):
+            # one persistent launch for every decode step (it stops on device once all rows finish)
+            df = self._df_decoder()
+            df.run(B, steps_max, repetition_penalty)
+            ev2.record()
+            lens = self.lens[:n].cpu().tolist()
+            toks = self.out_tokens[:n].cpu().numpy()
+            df.check()
+            res = [toks[b, : lens[b]].tolist() for b in range(n)]
+            if stats is not None:
+                ev2.synchronize()
+                stats.batch += n
+                stats.prompt_tokens += sum(len(p) for p in prompts)
+                stats.new_tokens += sum(lens[b] - len(prompts[b]) for b in range(n))
+                stats.prefill_ms += ev0.elapsed_time(ev1)
+                stats.decode_ms += ev1.elapsed_time(ev2)
+                stats.steps += steps_max
+                stats.graph = False
+            return res
         graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
         kg = self._steps_per_graph_for(B)
         if graph is None or self.check_every % kg:

@@ -31,7 +31,8 @@ CHECK_UNITS = ("gemm", "attention", "decode", "encoder", "skinny", "gemm_ps")
 CHECK_SITES = {1: "embed token id", 2: "position id", 3: "decode_update slot_map", 4: "decode_update token id",
                5: "decode_update sequence length", 6: "seen_set row", 7: "QKV scatter slot", 8: "QKV scatter position",
                9: "attention slot", 10: "BERT token id", 11: "seen_set token id"}
-SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip", "skinny.hip", "gemm_ps.hip"]
+SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip", "skinny.hip", "gemm_ps.hip",
+           "dataflow.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
 EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)

@@ -1,0 +1,296 @@
+"""Host side of the persistent dataflow decode (``ops/csrc/dataflow.hip``): per-CU work
+assignment, the per-CU packed weight streams, the device tables and the launch.
+
+One launch decodes up to ``nsteps`` greedy steps for 1-2 rows (the reference serves each
+student query with its own ``model.generate``: ``tutoring_server.py:21-29``).  Every CU owns
+fixed weight rows and streams exactly those, in the order it consumes them, from a private
+contiguous region of ``packed`` into an LDS ring; phases hand off through fresh-per-step
+counters and tagged granules in ``scratch``.  See the kernel file for the protocol.
+
+Work split over G CUs (``assign``; pure Python so CPU tests check it):
+  * W_qkv rows (3d), c_fc/c_proj pairs (4d) and LM-head rows (padded vocab) split evenly;
+  * each head's attention runs on ``GS`` CUs, each owning 64/GS head dims of W_o^T (so the
+    out-projection is an axpy of those rows by the head's attention output).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _check, _stream, lib
+
+P = ctypes.c_void_p
+
+
+class DfCu(ctypes.Structure):
+    _fields_ = [("q0", ctypes.c_int), ("nq", ctypes.c_int), ("f0", ctypes.c_int), ("nf", ctypes.c_int),
+                ("v0", ctypes.c_int), ("nv", ctypes.c_int), ("ah", ctypes.c_int), ("ak0", ctypes.c_int),
+                ("nk", ctypes.c_int), ("pad0", ctypes.c_int), ("pad1", ctypes.c_int), ("pad2", ctypes.c_int),
+                ("off", ctypes.c_longlong), ("step_bytes", ctypes.c_longlong)]
+
+
+class DfLayer(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("ln1_g", "ln1_b", "b_qkv", "b_o", "ln2_g", "ln2_b", "b_fc", "b_p",
+                                 "k_cache", "v_cache")]
+
+
+_INT_FIELDS = ("R", "D", "H", "L", "V", "T", "seen_words", "eos", "nsteps", "A", "C", "max_nq", "swl", "ring_bytes",
+               "ldx", "n_slots", "P", "nt_weights", "ko", "kf")
+
+
+class DfArgs(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("packed", "cus", "layers", "wte", "wpe", "lnf_g", "lnf_b", "lens", "finished",
+                                 "out_tokens", "seen", "cur_tok", "cur_pos", "cur_kvlen", "slots", "x_out",
+                                 "scratch", "err", "trace")] + \
+               [("step_words", ctypes.c_longlong)] + [(n, ctypes.c_int) for n in _INT_FIELDS] + \
+               [("exp_att", ctypes.c_int * 8), ("exp_mlp", ctypes.c_int * 8)] + \
+               [("eps", ctypes.c_float), ("penalty", ctypes.c_float)]
+
+
+LDS_MAX = 160 * 1024
+SUPPORTED_D = (128, 256, 768, 1024)  # larger d: the per-CU MLP region outgrows the ring (round 4)
+MAX_ROWS = 2
+ERRORS = {1: "arrival-counter wait timed out", 2: "q/k/v granule wait timed out", 3: "LDS hand-off wait timed out",
+          4: "weight loader timed out"}
+
+
+def _bind_once():
+    L = lib()
+    if getattr(L, "_df_bound", False):
+        return L
+    L.dlms_dataflow_decode.argtypes = [ctypes.POINTER(DfArgs), ctypes.c_int, P]
+    L.dlms_dataflow_decode.restype = ctypes.c_int
+    for n in ("dlms_df_args_size", "dlms_df_cu_size", "dlms_df_layer_size", "dlms_df_threads"):
+        getattr(L, n).restype = ctypes.c_int
+    L.dlms_df_lds_fixed.argtypes = [ctypes.c_int] * 4
+    L.dlms_df_lds_fixed.restype = ctypes.c_int
+    L.dlms_df_step_words.argtypes = [ctypes.c_int] * 4
+    L.dlms_df_step_words.restype = ctypes.c_longlong
+    for name, st in (("dlms_df_args_size", DfArgs), ("dlms_df_cu_size", DfCu), ("dlms_df_layer_size", DfLayer)):
+        if getattr(L, name)() != ctypes.sizeof(st):
+            raise RuntimeError(f"{name}: ctypes mirror and compiled library disagree")
+    L._df_bound = True
+    return L
+
+
+def split_even(n: int, parts: int, i: int) -> tuple[int, int]:
+    base, rem = divmod(n, parts)
+    return i * base + min(i, rem), base + (1 if i < rem else 0)
+
+
+def pad16(n: int) -> int:
+    return max(16, -(-n // 16) * 16)
+
+
+ROW_PAD = 16  # bf16 elements of padding per streamed row (dataflow.hip ROW_BYTES)
+
+
+@dataclass
+class CuPlan:
+    q0: int
+    nq: int
+    f0: int
+    nf: int
+    v0: int
+    nv: int
+    ah: int = -1
+    ak0: int = 0
+    nk: int = 0
+
+    def layer_elems(self, d: int, ko: int, kf: int) -> int:
+        """bf16 elements of one layer in the stream: W_qkv rows (padded), the K-major W_o block
+        [d][ko] (attention CUs), the c_fc rows (padded), the K-major c_proj block [d][kf]."""
+        return (self.nq + self.nf) * (d + ROW_PAD) + (d * ko if self.nk else 0) + d * kf
+
+    def step_elems(self, L: int, d: int, ko: int, kf: int) -> int:
+        return L * self.layer_elems(d, ko, kf) + self.nv * (d + ROW_PAD)
+
+
+def block_k(cus: list[CuPlan]) -> tuple[int, int]:
+    """(ko, kf): K of the W_o / c_proj blocks, padded to the 16-deep MFMA step (same for all CUs)."""
+    nk = max((cu.nk for cu in cus), default=0)
+    return pad16(nk), pad16(max(cu.nf for cu in cus))
+
+
+def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int) -> list[CuPlan]:
+    """Work of each of G CUs (see module docstring).  Attention CU a = h * GS + g sits at CU
+    (a * G) // A, spreading the A = n_head * GS attention CUs over all XCDs."""
+    if 64 % GS or n_head * GS > G:
+        raise ValueError(f"dataflow: GS={GS} must divide 64 and n_head * GS <= {G}")
+    cus = []
+    for c in range(G):
+        q0, nq = split_even(3 * d, G, c)
+        f0, nf = split_even(n_inner, G, c)
+        v0, nv = split_even(vocab_padded, G, c)
+        cus.append(CuPlan(q0, nq, f0, nf, v0, nv))
+    A = n_head * GS
+    nk = 64 // GS
+    for a in range(A):
+        cu = cus[(a * G) // A]
+        cu.ah, cu.ak0, cu.nk = a // GS, (a % GS) * nk, nk
+    return cus
+
+
+def kmajor_blocks(w: torch.Tensor, cols: list[list[int]], K: int) -> torch.Tensor:
+    """w [d, n] -> [len(cols), d, K]: block c = w[:, cols[c]] zero-padded to K columns."""
+    d = w.shape[0]
+    ext = torch.cat([w, torch.zeros(d, 1, dtype=w.dtype, device=w.device)], dim=1)
+    idx = torch.full((len(cols), K), w.shape[1], dtype=torch.long)
+    for c, cc in enumerate(cols):
+        idx[c, : len(cc)] = torch.tensor(cc, dtype=torch.long)
+    return ext[:, idx.to(w.device).reshape(-1)].reshape(d, len(cols), K).permute(1, 0, 2).contiguous()
+
+
+def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]:
+    """Every CU's stream in one flat bf16 buffer, in the order the kernel consumes it: per layer
+    [W_qkv rows | W_o block | c_fc rows | c_proj block], then its LM-head rows (rows padded by
+    ROW_PAD).  Returns the buffer and each CU's first element."""
+    cfg = w.cfg
+    d, L = cfg.n_embd, cfg.n_layer
+    ko, kf = block_k(cus)
+    G = len(cus)
+    sizes = [cu.step_elems(L, d, ko, kf) for cu in cus]
+    starts = np.cumsum([0] + sizes)[:-1].tolist()
+    packed = torch.zeros(sum(sizes), dtype=torch.bfloat16, device=device)
+    pad = lambda t: torch.nn.functional.pad(t, (0, ROW_PAD))  # noqa: E731
+    o_cols = [[cu.ah * 64 + cu.ak0 + k for k in range(cu.nk)] for cu in cus]
+    p_cols = [[cu.f0 + i for i in range(cu.nf)] for cu in cus]
+    for l, lw in enumerate(w.layers):
+        qkv, fc = pad(lw.w_qkv), pad(lw.w_fc)
+        ob = kmajor_blocks(lw.w_o, o_cols, ko).reshape(G, -1)
+        pb = kmajor_blocks(lw.w_p, p_cols, kf).reshape(G, -1)
+        for c, cu in enumerate(cus):
+            o = starts[c] + l * cu.layer_elems(d, ko, kf)
+            for piece in (qkv[cu.q0: cu.q0 + cu.nq].reshape(-1), ob[c] if cu.nk else None,
+                          fc[cu.f0: cu.f0 + cu.nf].reshape(-1), pb[c]):
+                if piece is None:
+                    continue
+                packed[o: o + piece.numel()].copy_(piece)
+                o += piece.numel()
+    lm = pad(w.wte)
+    for c, cu in enumerate(cus):
+        o = starts[c] + L * cu.layer_elems(d, ko, kf)
+        packed[o: o + cu.nv * (d + ROW_PAD)].copy_(lm[cu.v0: cu.v0 + cu.nv].reshape(-1))
+    return packed, starts
+
+
+class DataflowDecoder:
+    """Persistent dataflow decode bound to one ``HipGPT2Engine`` (TP=1, bf16, 1-2 rows)."""
+
+    COPIES = 2  # fixed-point residual copies (workgroup c adds into copy c % COPIES)
+
+    @staticmethod
+    def supported(eng) -> bool:
+        cfg = eng.cfg
+        return (eng.tp_size == 1 and not eng.w.fp8 and cfg.n_embd in SUPPORTED_D and cfg.n_embd == 64 * cfg.n_head
+                and eng.w.ffn_local == 4 * cfg.n_embd)
+
+    def __init__(self, eng, grid: int | None = None, gs: int | None = None):
+        if not self.supported(eng):
+            raise ValueError("dataflow decode: TP=1 bf16 GPT-2 with d in %s only" % (SUPPORTED_D,))
+        self.L = _bind_once()
+        self.eng = eng
+        cfg, dev = eng.cfg, eng.device
+        props = torch.cuda.get_device_properties(dev)
+        G = grid or int(os.environ.get("DLMS_DF_GRID", "0")) or min(int(props.multi_processor_count), 256)
+        gs = gs or int(os.environ.get("DLMS_DF_GS", "4"))
+        while cfg.n_head * gs > G and gs > 1:
+            gs //= 2
+        self.G, self.GS = G, gs
+        self.cus = assign(cfg.n_embd, cfg.n_head, eng.w.ffn_local, cfg.vocab_padded, G, gs)
+        self.A = cfg.n_head * gs
+        self.ko, self.kf = block_k(self.cus)
+        if self.ko > 64 or self.kf > 64:
+            raise ValueError("dataflow: more than 64 c_proj / W_o columns per CU")
+        self.packed, starts = pack_weights(eng.w, self.cus, dev)
+        D = cfg.n_embd
+        self.max_nq = max(cu.nq for cu in self.cus)
+        if self.max_nq > 64:
+            raise ValueError("dataflow: more than 64 W_qkv rows per CU")
+        max_nv = max(cu.nv for cu in self.cus)
+        self.swl = -(-max_nv // 64) * 2 + 2
+        tab = (DfCu * G)()
+        for c, cu in enumerate(self.cus):
+            tab[c] = DfCu(cu.q0, cu.nq, cu.f0, cu.nf, cu.v0, cu.nv, cu.ah, cu.ak0, cu.nk, 0, 0, 0,
+                          starts[c] * 2, cu.step_elems(cfg.n_layer, D, self.ko, self.kf) * 2)
+        self.max_step_bytes = max(cu.step_elems(cfg.n_layer, D, self.ko, self.kf) for cu in self.cus) * 2
+        self.cu_tab = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
+        lt = (DfLayer * cfg.n_layer)()
+        for l, lw in enumerate(eng.w.layers):
+            lt[l] = DfLayer(lw.ln1_g.data_ptr(), lw.ln1_b.data_ptr(), lw.b_qkv.data_ptr(), lw.b_o.data_ptr(),
+                            lw.ln2_g.data_ptr(), lw.ln2_b.data_ptr(), lw.b_fc.data_ptr(), lw.b_p.data_ptr(),
+                            eng.kv[l, 0].data_ptr(), eng.kv[l, 1].data_ptr())
+        self.layer_tab = torch.frombuffer(bytearray(bytes(lt)), dtype=torch.uint8).to(dev)
+        self.err = torch.zeros(16, dtype=torch.int32, device=dev)
+        self._scratch: dict[int, torch.Tensor] = {}
+        self.slots = torch.arange(MAX_ROWS, dtype=torch.int32, device=dev)
+
+    def ring_bytes(self, R: int) -> int:
+        fixed = self.L.dlms_df_lds_fixed(self.eng.cfg.n_embd, R, self.max_nq, self.swl)
+        return (LDS_MAX - fixed) // 8192 * 8192  # a multiple of the loader's 8 KiB batches
+
+    def step_words(self, R: int) -> int:
+        return int(self.L.dlms_df_step_words(R, self.eng.cfg.n_embd, self.eng.cfg.n_layer, self.COPIES))
+
+    def _scratch_for(self, R: int, nsteps: int) -> torch.Tensor:
+        words = self.step_words(R) * nsteps
+        buf = self._scratch.get(R)
+        if buf is None or buf.numel() < words:
+            cap = self.step_words(R) * max(nsteps, self.eng.max_length)
+            buf = torch.empty(cap, dtype=torch.int64, device=self.eng.device)
+            self._scratch[R] = buf
+        return buf
+
+    TRACE_STEPS, TRACE_EV = 4, 32  # dataflow.hip TR_STEPS / TR_EV
+
+    def trace_buffer(self) -> torch.Tensor:
+        """A zeroed stamp buffer for ``run(trace=...)``: [G, TRACE_STEPS, L + 1, TRACE_EV] int64
+        wall-clock ticks (100 MHz) of each CU's comm wave at fixed points of every phase."""
+        L = self.eng.cfg.n_layer
+        return torch.zeros(self.G, self.TRACE_STEPS, L + 1, self.TRACE_EV, dtype=torch.int64, device=self.eng.device)
+
+    def run(self, B: int, nsteps: int, penalty: float, x_out: bool = True, trace: torch.Tensor | None = None):
+        """``nsteps`` greedy decode steps (at most) of rows [0, B), B <= 2, on the current stream:
+        exactly the state transitions of ``nsteps`` launch-per-op steps (decode_update semantics),
+        stopping early once every row has finished."""
+        eng, cfg = self.eng, self.eng.cfg
+        if not 1 <= B <= MAX_ROWS or nsteps <= 0:
+            raise ValueError(f"dataflow run: B in [1, {MAX_ROWS}], nsteps > 0")
+        if nsteps * self.max_step_bytes >= 2 ** 32 - 2 ** 24:
+            raise ValueError("dataflow run: too many steps for one launch (32-bit stream offsets)")
+        scratch = self._scratch_for(B, nsteps)
+        sw = self.step_words(B)
+        scratch[: sw * nsteps].zero_()
+        self.err.zero_()
+        a = DfArgs()
+        w = eng.w
+        for name, t in (("packed", self.packed), ("cus", self.cu_tab), ("layers", self.layer_tab), ("wte", w.wte),
+                        ("wpe", w.wpe), ("lnf_g", w.lnf_g), ("lnf_b", w.lnf_b), ("lens", eng.lens),
+                        ("finished", eng.finished), ("out_tokens", eng.out_tokens), ("seen", eng.seen),
+                        ("cur_tok", eng.cur_tok), ("cur_pos", eng.cur_pos), ("cur_kvlen", eng.cur_kvlen),
+                        ("slots", self.slots), ("scratch", scratch), ("err", self.err)):
+            setattr(a, name, t.data_ptr())
+        a.x_out = eng.x.data_ptr() if x_out else None
+        a.trace = trace.data_ptr() if trace is not None else None
+        a.step_words = sw
+        a.R, a.D, a.H, a.L = B, cfg.n_embd, cfg.n_head, cfg.n_layer
+        a.V, a.T, a.seen_words, a.eos = cfg.vocab_size, eng.max_length, eng.seen_words, cfg.eos_token_id
+        a.nsteps, a.A, a.C, a.max_nq, a.swl = nsteps, self.A, self.COPIES, self.max_nq, self.swl
+        a.ring_bytes, a.ldx, a.n_slots, a.P = self.ring_bytes(B), eng.x.stride(0), eng.max_batch, cfg.n_positions
+        a.eps, a.penalty = cfg.layer_norm_epsilon, float(penalty)
+        a.nt_weights = int(os.environ.get("DLMS_DF_NT", "0") == "1")
+        a.ko, a.kf = self.ko, self.kf
+        for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
+            a.exp_mlp[c] = sum(1 for i in range(self.G) if i % self.COPIES == c)
+            a.exp_att[c] = sum(1 for i, cu in enumerate(self.cus) if cu.nk and i % self.COPIES == c)
+        _check(self.L.dlms_dataflow_decode(ctypes.byref(a), self.G, _stream()), "dlms_dataflow_decode")
+
+    def check(self):
+        """Raise if the last launch gave up on a hand-off (synchronises)."""
+        e = self.err[:4].cpu().tolist()
+        if e[0]:
+            raise RuntimeError(f"dataflow decode: {ERRORS.get(e[0], e[0])} (block {e[1]}, step {e[2]}, site {e[3]})")
