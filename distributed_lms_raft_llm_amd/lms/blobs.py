@@ -138,9 +138,53 @@ class BlobStore:
             self.put_chunks(sha, [data])
         return sha
 
-    def put_chunks(self, sha: str, chunks, fsync: bool = False) -> bool:
+    def get_sha(self, sha: str, relpath: str | None = None, fetch_timeout: float = 30.0) -> bytes:
+        """Bytes of CAS object ``sha`` (an entry's own upload: two same-named uploads keep their
+        own bytes), pulled from a peer if this replica does not hold it; ``relpath`` is the
+        fallback for entries recorded before uploads carried their sha."""
+        if is_sha256(sha):
+            for attempt in range(2):
+                try:
+                    with open(self.cas_path(sha), "rb") as f:
+                        return f.read()
+                except FileNotFoundError:
+                    if attempt or self.fetcher is None or not self.fetcher.fetch(sha, timeout=fetch_timeout):
+                        break
+        return self.get(relpath, sha) if relpath else b""
+
+    def gc(self, referenced: set[str], grace_s: float = 600.0) -> int:
+        """Delete CAS objects no replicated entry references any more (snapshot time).  Objects
+        younger than ``grace_s`` survive: a pre-replicated upload whose PutBlob has not committed
+        yet is unreferenced but live.  ``uploads/<name>`` links keep their own inode.  Returns the
+        number of objects removed."""
+        d = os.path.join(self.root, CAS_FOLDER)
+        now = time.time()
+        removed = 0
+        for name in os.listdir(d):
+            if not is_sha256(name) or name in referenced:
+                continue
+            path = os.path.join(d, name)
+            try:
+                if now - os.path.getmtime(path) >= grace_s:
+                    os.unlink(path)
+                    removed += 1
+            except FileNotFoundError:
+                pass
+        return removed
+
+    def _fsync_dir(self, path: str):
+        fd = os.open(os.path.dirname(path), os.O_RDONLY)
+        try:
+            os.fsync(fd)
+        finally:
+            os.close(fd)
+
+    def put_chunks(self, sha: str, chunks, fsync: bool = True) -> bool:
         """Write an object from an iterable of byte chunks; verified against ``sha`` before it
-        becomes visible (a torn or corrupted transfer never lands).  Idempotent."""
+        becomes visible (a torn or corrupted transfer never lands).  Idempotent.  ``fsync``
+        (default): the file AND its directory entry are on disk before this returns -- a
+        replica acknowledges a pre-replication push only then, so "a majority holds the blob"
+        survives a crash just like the log entry that depends on it."""
         path = self.cas_path(sha)
         if os.path.exists(path):
             for _ in chunks:  # drain the stream
@@ -159,6 +203,8 @@ class BlobStore:
             if h.hexdigest() != sha:
                 raise ValueError(f"blob content does not match {sha[:12]}")
             os.replace(tmp, path)
+            if fsync:
+                self._fsync_dir(path)
             return True
         finally:
             if os.path.exists(tmp):

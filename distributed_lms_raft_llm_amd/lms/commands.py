@@ -25,7 +25,9 @@ legacy ``StoreBlob`` [filename, sha256, base64] (still applied when replaying ol
 
 An optional top-level ``"rid"`` (client request id) makes a write idempotent: the state machine
 applies a given rid once and answers retries with the first result (a client that retries a
-write after a leader failover must not post the same assignment twice).
+write after a leader failover must not post the same assignment twice).  An optional top-level
+``"sha256"`` on ``PostAssignment`` / ``PostCourseMaterial`` names the entry's own upload (its
+CAS object), so two same-named uploads keep their own bytes; ``args`` stay the reference's.
 
 ``decode`` also accepts the reference's shadowed legacy encoder (``lms_server.py:317-333``):
 ``Op arg1 "multi word arg" ...`` (shlex quoting).
@@ -51,7 +53,10 @@ class BadCommand(ValueError):
     pass
 
 
-def encode(operation: str, args: list, rid: str | None = None) -> str:
+META_KEYS = ("sha256",)
+
+
+def encode(operation: str, args: list, rid: str | None = None, meta: dict | None = None) -> str:
     if operation not in ALL_OPS:
         raise BadCommand(f"unknown operation {operation!r}")
     if len(args) != ALL_OPS[operation]:
@@ -59,7 +64,23 @@ def encode(operation: str, args: list, rid: str | None = None) -> str:
     obj = {"operation": operation, "args": list(args)}
     if rid:
         obj["rid"] = str(rid)
+    for k, v in (meta or {}).items():
+        if k not in META_KEYS:
+            raise BadCommand(f"unknown command field {k!r}")
+        obj[k] = v
     return json.dumps(obj)
+
+
+def decode_meta(command: str) -> dict:
+    """The optional top-level fields (``META_KEYS``) of a JSON command ({} for the legacy form)."""
+    s = command.strip()
+    if not s.startswith("{"):
+        return {}
+    try:
+        obj = json.loads(s)
+    except ValueError:
+        return {}
+    return {k: obj[k] for k in META_KEYS if k in obj}
 
 
 def decode(command: str) -> tuple[str, list]:

@@ -91,10 +91,19 @@ def extract_text(data: bytes, limit: int | None = None) -> str:
     for mod in ("pypdf", "PyPDF2"):
         try:
             lib = __import__(mod)
-            reader = lib.PdfReader(io.BytesIO(data))
-            return "".join((p.extract_text() or "") for p in reader.pages)
         except ImportError:
             continue
+        try:
+            reader = lib.PdfReader(io.BytesIO(data))
+            parts, total = [], 0
+            for page in reader.pages:  # stop parsing once the cap is reached (leader request path)
+                t = page.extract_text() or ""
+                parts.append(t)
+                total += len(t)
+                if limit is not None and total >= limit:
+                    break
+            out = "".join(parts)
+            return out if limit is None else out[:limit]
         except Exception:
             break
     return _builtin_extract(data, limit)

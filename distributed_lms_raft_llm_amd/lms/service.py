@@ -165,9 +165,11 @@ class LMSServicer:
     def _write(self, op: str, args: list, rid: str | None = None):
         return self.node.propose(commands.encode(op, args, rid), timeout=self.write_timeout)
 
-    def _write_many(self, items: list[tuple[str, list]], rid: str | None = None):
-        futs = [self.node.submit(commands.encode(op, a, f"{rid}.{k}" if rid else None))
-                for k, (op, a) in enumerate(items)]
+    def _write_many(self, items: list[tuple], rid: str | None = None):
+        """(operation, args[, meta]) items proposed back to back."""
+        futs = [self.node.submit(commands.encode(it[0], it[1], f"{rid}.{k}" if rid else None,
+                                                 it[2] if len(it) > 2 else None))
+                for k, it in enumerate(items)]
         return [f.result(timeout=self.write_timeout) for f in futs]
 
     def _read_fence(self):
@@ -214,9 +216,13 @@ class LMSServicer:
         user = self.state.read(lambda d: dict(d["users"][request.username]) if request.username in d["users"] else None)
         if user is None or user["password"] != request.password:
             return pb.LoginResponse(success=False)
-        token = str(uuid.uuid4())
+        # with a client request id the token is derived from it, so a retried Login (reply lost)
+        # is deduplicated by the state machine and returns the SAME session instead of minting a
+        # second one
+        rid = self._rid(context)
+        token = str(uuid.uuid5(uuid.NAMESPACE_URL, f"dlms-login/{request.username}/{rid}")) if rid else str(uuid.uuid4())
         try:
-            self._write("Login", [request.username, token, user["role"]])
+            self._write("Login", [request.username, token, user["role"]], rid)
         except Exception:
             return pb.LoginResponse(success=False)
         return pb.LoginResponse(success=True, token=token, role=user["role"])
@@ -225,10 +231,15 @@ class LMSServicer:
         fwd = self._forward("Logout", request, context)
         if fwd is not None:
             return fwd
+        rid = self._rid(context)
+        self._read_fence()
+        done, first = self.state.rid_result(rid)
+        if done:  # a retry of a Logout that already committed: the same answer
+            return pb.LogoutResponse(success=bool(first))
         if self._session(request.token) is None:
             return pb.LogoutResponse(success=False)
         try:
-            ok = self._write("Logout", [request.token])
+            ok = self._write("Logout", [request.token], rid)
         except Exception:
             return pb.LogoutResponse(success=False)
         return pb.LogoutResponse(success=bool(ok))
@@ -244,17 +255,21 @@ class LMSServicer:
         user, role = s["username"], s["role"]
         rid = self._rid(context)
         try:
+            # (the entry carries its upload's sha as a command field: a later same-named upload
+            # replaces uploads/<name> but not what this entry downloads)
             if role == "instructor" and request.type == "course_material":
                 path = self.state.blobs.relpath(request.filename)
-                self._write_many([self._store_upload(request.filename, bytes(request.file)),
-                                  ("PostCourseMaterial", [user, request.filename, path])], rid)
+                put = self._store_upload(request.filename, bytes(request.file))
+                self._write_many([put, ("PostCourseMaterial", [user, request.filename, path],
+                                        {"sha256": put[1][1]})], rid)
                 return pb.PostResponse(success=True)
             if role == "student" and request.type == "assignment":
                 blob = bytes(request.file)
                 text = extract_text(blob, TEXT_CAP)
                 path = self.state.blobs.relpath(request.filename)
-                self._write_many([self._store_upload(request.filename, blob),
-                                  ("PostAssignment", [user, request.filename, path, text])], rid)
+                put = self._store_upload(request.filename, blob)
+                self._write_many([put, ("PostAssignment", [user, request.filename, path, text],
+                                        {"sha256": put[1][1]})], rid)
                 return pb.PostResponse(success=True)
             if role == "student" and request.type == "query":
                 self._write("AskQuery", [user, request.data], rid)
@@ -272,17 +287,18 @@ class LMSServicer:
             return pb.GetResponse(success=False)
         self._read_fence()
         if request.type == "course_material" and s["role"] == "student":
-            mats = self.state.read(lambda d: [(m["filename"], m["filepath"], m.get("instructor", "Unknown"))
-                                              for m in d["course_materials"]])
+            mats = self.state.read(lambda d: [(m["filename"], m["filepath"], m.get("instructor", "Unknown"),
+                                               m.get("sha256")) for m in d["course_materials"]])
             if not mats:
                 return pb.GetResponse(success=True, message=MSG_NO_MATERIALS)
             return pb.GetResponse(success=True, entries=[
-                pb.DataEntry(id="1", filename=f, file=self.state.read_blob(p), instructor=ins) for f, p, ins in mats])
+                pb.DataEntry(id="1", filename=f, file=self.state.read_blob(p, sha), instructor=ins)
+                for f, p, ins, sha in mats])
         if s["role"] == "instructor" and request.type == "student_list":
-            rows = self.state.read(lambda d: [(st, a["filename"], a["filepath"]) for st, items in d["assignments"].items()
-                                              for a in items])
+            rows = self.state.read(lambda d: [(st, a["filename"], a["filepath"], a.get("sha256"))
+                                              for st, items in d["assignments"].items() for a in items])
             return pb.GetResponse(success=True, entries=[
-                pb.DataEntry(id=st, filename=f, file=self.state.read_blob(p)) for st, f, p in rows])
+                pb.DataEntry(id=st, filename=f, file=self.state.read_blob(p, sha)) for st, f, p, sha in rows])
         return pb.GetResponse(success=False, message=MSG_BAD_GET)
 
     def GradeAssignment(self, request, context):
@@ -379,6 +395,12 @@ class LMSServicer:
         assignment_text = self.state.read(
             lambda d: d["assignments"][user][0]["text"] if d["assignments"].get(user) else None)
         if assignment_text is None:
+            # a follower may not have applied an assignment its leader just committed: ask the
+            # leader (which fences its reads) before answering "no assignment"
+            if not self.node.is_leader:
+                fwd = self._forward("GetLLMAnswer", request, context)
+                if fwd is not None:
+                    return fwd
             return pb.QueryResponse(success=True, response=MSG_LLM_NO_ASSIGNMENT)
         if self.gate is not None:
             tg = time.perf_counter()

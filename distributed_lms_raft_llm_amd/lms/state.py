@@ -32,11 +32,14 @@ import copy
 import hashlib
 import json
 import os
+import logging
 import threading
 from collections import OrderedDict
 
 from . import commands
 from .blobs import UPLOAD_FOLDER, BlobStore, safe_filename  # noqa: F401  (re-exported)
+
+log = logging.getLogger("dlms.lms.state")
 
 DATABASE_FILE = "lms_data.json"
 DEDUPE_CAP = 20000  # client request ids remembered (oldest evicted first, identically on every replica)
@@ -92,9 +95,24 @@ class LMSState:
         """The replicated state as JSON -- blob BYTES are not included (``blob_index`` names each
         upload's CAS object; a restoring replica pulls what it lacks from its peers)."""
         with self.lock:
-            return json.dumps({"data": self.data, "sessions": self.sessions, "kv": self.kv,
+            snap = json.dumps({"data": self.data, "sessions": self.sessions, "kv": self.kv,
                                "applied_index": self.applied_index, "blob_index": self.blob_index,
                                "dedupe": list(self.dedupe.items())})
+        # the log prefix this snapshot replaces is the last thing that could name an object the
+        # state no longer references: collect those CAS objects now (off the caller's thread)
+        refs = self.referenced_blobs()
+        threading.Thread(target=self._gc, args=(refs,), daemon=True, name="blob-gc").start()
+        return snap
+
+    gc_grace_s = 600.0  # unreferenced objects younger than this survive (uploads in flight)
+
+    def _gc(self, refs: set[str]):
+        try:
+            n = self.blobs.gc(refs, self.gc_grace_s)
+            if n:
+                log.info("blob gc: removed %d unreferenced object(s)", n)
+        except OSError as e:
+            log.warning("blob gc failed: %s", e)
 
     def restore(self, snap: str):
         obj = json.loads(snap) if snap else {}
@@ -132,9 +150,21 @@ class LMSState:
         with self.lock:
             return self.blob_index.get(relpath)
 
-    def read_blob(self, relpath: str) -> bytes:
-        """An upload's bytes (fetched from a peer first if this replica does not hold them)."""
+    def read_blob(self, relpath: str, sha: str | None = None) -> bytes:
+        """An upload's bytes (fetched from a peer first if this replica does not hold them):
+        by the entry's own sha when it has one, else the latest upload under that name."""
+        if sha:
+            return self.blobs.get_sha(sha, relpath)
         return self.blobs.get(relpath, self.blob_sha(relpath))
+
+    def referenced_blobs(self) -> set[str]:
+        """Every CAS object the replicated state still points at (snapshot-time GC)."""
+        with self.lock:
+            refs = set(self.blob_index.values())
+            for items in self.data.get("assignments", {}).values():
+                refs.update(a["sha256"] for a in items if a.get("sha256"))
+            refs.update(m["sha256"] for m in self.data.get("course_materials", []) if m.get("sha256"))
+        return refs
 
     # ------------------------------------------------------------------ apply
     def apply(self, index: int, command: str):
@@ -149,8 +179,9 @@ class LMSState:
             fn = getattr(self, "_op_" + op, None)
             if fn is None:
                 return None
+            meta = commands.decode_meta(command) if op in ("PostAssignment", "PostCourseMaterial") else {}
             try:
-                res = fn(*args)
+                res = fn(*args, **meta)
             except TypeError:  # wrong arity from a foreign/legacy writer: ignore the entry
                 return None
             if rid is not None:
@@ -174,14 +205,24 @@ class LMSState:
         users[username] = {"password": password, "role": role}
         return True
 
-    def _op_PostAssignment(self, student, filename, file_path, assignment_text):
-        self.data.setdefault("assignments", {}).setdefault(student, []).append({
-            "filename": filename, "filepath": self.blobs.relpath(filename), "grade": None, "text": assignment_text})
+    # (the reference's argument order; ``sha256`` -- the command's top-level field, lms/commands.py
+    # -- keys the entry to ITS upload, so a later same-named upload does not change its download)
+    def _op_PostAssignment(self, student, filename, file_path, assignment_text, sha256=None):
+        rel = self.blobs.relpath(filename)
+        entry = {"filename": filename, "filepath": rel, "grade": None, "text": assignment_text}
+        sha = sha256 if isinstance(sha256, str) and len(sha256) == 64 else self.blob_index.get(rel)
+        if sha:
+            entry["sha256"] = sha
+        self.data.setdefault("assignments", {}).setdefault(student, []).append(entry)
         return True
 
-    def _op_PostCourseMaterial(self, instructor, filename, file_path):
-        self.data.setdefault("course_materials", []).append({
-            "filename": filename, "filepath": self.blobs.relpath(filename), "instructor": instructor})
+    def _op_PostCourseMaterial(self, instructor, filename, file_path, sha256=None):
+        rel = self.blobs.relpath(filename)
+        entry = {"filename": filename, "filepath": rel, "instructor": instructor}
+        sha = sha256 if isinstance(sha256, str) and len(sha256) == 64 else self.blob_index.get(rel)
+        if sha:
+            entry["sha256"] = sha
+        self.data.setdefault("course_materials", []).append(entry)
         return True
 
     def _op_AskQuery(self, username, query):

@@ -10,13 +10,13 @@
 // that needs them, and the phases hand off through per-phase arrival counters instead of kernel
 // boundaries or grid barriers.
 //
-// Geometry: one 384-thread workgroup per CU (G <= #CUs, all resident: ~160 KB of LDS each):
+// Geometry: one 448-thread workgroup per CU (G <= #CUs, all resident: ~160 KB of LDS each):
 //   wave 0      "comm": polls arrival counters / granules, loads the residual, LayerNorm, publishes
 //               results (granule stores, 64-bit fixed-point atomics, counter adds).  It is the only
 //               wave that waits on vmcnt for hand-off traffic.
-//   wave 1      "loader": streams this CU's pre-packed weight rows (global -> LDS ring by LDS-DMA,
+//   waves 1-2   "loaders": stream this CU's pre-packed weight rows (global -> LDS ring by LDS-DMA,
 //               global_load_lds_dwordx4), as far ahead as the ring allows.
-//   waves 2..5  "compute": MFMA on the ring's weight rows: v_mfma_f32_16x16x32_bf16 for the
+//   waves 3..6  "compute": MFMA on the ring's weight rows: v_mfma_f32_16x16x32_bf16 for the
 //               dot-product phases (row-major rows ARE the B fragments), v_mfma_f32_16x16x16_bf16
 //               on K-major blocks for the out-projection / c_proj (each wave owns 16-column
 //               output tiles, so no cross-wave reduction); attention for the CU's head (K/V
@@ -47,12 +47,16 @@
 namespace df {
 
 constexpr int NC = 4;                 // compute waves
-constexpr int NWAVES = NC + 2;        // + comm + loader
+constexpr int NL = 2;                 // loader waves
+constexpr int NWAVES = NC + NL + 1;   // + comm
 constexpr int NTHREADS = 64 * NWAVES;
 constexpr int SHARDS = 8;             // arrival counters are sharded by blockIdx % 8
 constexpr int CSTRIDE = 16;           // u64 words between shards (one 128-B line each)
-constexpr int INFL = 32;              // LDS-DMA units (1 KiB) in flight per loader wave
-constexpr int COPIES = 2;             // fixed-point residual copies (CU c adds into copy c % COPIES)
+constexpr int INFL = 48;              // LDS-DMA units (1 KiB) in flight per loader wave
+#ifndef DF_COPIES
+#define DF_COPIES 2
+#endif
+constexpr int COPIES = DF_COPIES;     // fixed-point residual copies (CU c adds into copy c % COPIES)
 constexpr int LDS_MAX = 160 * 1024;
 // a streamed weight row: d bf16 + 32 bytes of padding, so the 16 rows of an MFMA B fragment sit on
 // distinct 16-B LDS slots (a 1536-B row is 0 mod 256 B: 8-way ds_read_b128 conflicts unpadded)
@@ -133,7 +137,8 @@ __host__ __device__ inline Lay lds_layout(int D, int R, int max_nq, int swl, int
 }
 
 // ctl words
-enum { C_READY = 0, C_LOADED = 1, C_ABORT = 2, C_DONE = 3, C_CONT = 4, C_PHDONE = 16, C_CONS = 24, C_MID = 32 };
+enum { C_READY = 0, C_ABORT = 2, C_DONE = 3, C_CONT = 4, C_LOADED = 8, C_PHDONE = 16, C_CONS = 24, C_MID = 32 };
+// (C_LOADED + j: loader wave j's completed-batch count)
 // row state words (st[b * 8 + k])
 enum { S_TOK = 0, S_POS = 1, S_FIN = 2, S_LEN = 3, S_SLOT = 4 };
 // error codes
@@ -311,6 +316,30 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
 #pragma unroll
     for (int c = 0; c < COPIES; ++c) ec[c] = expc[c];
     const u64 t0 = clk();
+    // phase 1: poll ONE word per copy -- the element every producer adds last (row R-1, element
+    // D-1) -- so 256 pollers do not hammer the lines the atomics are still updating
+    for (;;) {
+        bool done = true;
+        if (lane < COPIES) {
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, ((lane * R + R - 1) * D + D - 1) * 8, 0, 16);
+            int want = ec[0];
+#pragma unroll
+            for (int c = 1; c < COPIES; ++c) want = lane == c ? ec[c] : want;
+            done = (int)(x[1] >> 24) == want;
+        }
+        if (__all(done)) break;
+        if ((unsigned)__builtin_amdgcn_readfirstlane((int)gld32(a.err)) || lds_ld(ctl + C_ABORT)) {
+            lds_st(ctl + C_ABORT, 1u);
+            return false;
+        }
+        if (clk() - t0 > TIMEOUT_TICKS) {
+            set_err(a, E_WAIT_CNT, where, s);
+            lds_st(ctl + C_ABORT, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    // phase 2: the whole buffer (almost always complete by now)
     for (;;) {
         u64 v[COPIES][R][EPL];
 #pragma unroll
@@ -644,37 +673,41 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
     lds_st(ctl + C_DONE, 1u);
 }
 
-// ------------------------------------------------------------------ loader wave
-// Streams this CU's row stream into the ring in batches of LB x 1 KiB LDS-DMA units (one
-// global_load_lds_dwordx4 each), keeping up to INFL units in flight; a batch is issued only when
-// every compute wave has released the ring bytes it overwrites.  One unit per loop iteration
-// capped the loader at ~10 GB/s per CU (the loop's LDS round trips), too slow for the LM head.
+// ------------------------------------------------------------------ loader waves
+// NL waves stream this CU's row stream into the ring in batches of LB x 1 KiB LDS-DMA units (one
+// global_load_lds_dwordx4 each); wave j issues batches j, j + NL, ..., keeping up to INFL units in
+// flight, and publishes how many of ITS batches have landed.  A batch is issued only when every
+// compute wave has released the ring bytes it overwrites.  (One wave issuing one unit per loop
+// iteration capped the loader at ~10 GB/s per CU; the LM head's ~300 KB per CU per step needs
+// far more in flight.)
 constexpr int LB = 8;  // units per batch (the ring is a multiple of LB KiB)
+constexpr unsigned BATCH = LB * 1024u;
 template <bool NT>
-__device__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int lane) {
+__device__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int j, int lane) {
     unsigned* ctl = reinterpret_cast<unsigned*>(lds + ly.ctl);
     const unsigned RB = (unsigned)a.ring_bytes;
     const unsigned SB = (unsigned)cu.step_bytes;
     const unsigned total = SB * (unsigned)a.nsteps;  // host guarantees < 2^32
+    const unsigned nbatch = (total + BATCH - 1) / BATCH;
     const char* base = reinterpret_cast<const char*>(a.packed) + cu.off;
     char* ring = lds + ly.ring;
-    unsigned u = 0;     // units issued (1 KiB each)
-    unsigned gpos = 0;  // step-local byte offset of unit u (lane 0's address)
-    unsigned rpos = 0;  // ring offset of unit u
-    unsigned published = 0;
+    unsigned k = 0;          // this wave's batches issued (its batch k is global batch j + NL k)
+    unsigned published = 0;  // ... and published as landed
     u64 t0 = clk();
-    while (u * 1024u < total) {
+    for (;;) {
+        const unsigned b = (unsigned)j + NL * k;
+        if (b >= nbatch) break;
         unsigned cons = 0xffffffffu;
 #pragma unroll
         for (int w = 0; w < NC; ++w) {
             const unsigned c = lds_ld(ctl + C_CONS + w);
             cons = c < cons ? c : cons;
         }
-        if ((u + LB) * 1024u > cons * 16u + RB) {  // ring full: publish everything, then wait
+        if ((b + 1) * BATCH > cons * 16u + RB) {  // ring full: publish everything, then wait
             drain();
-            if (published != u) {
-                published = u;
-                lds_st(ctl + C_LOADED, u * 64u);
+            if (published != k) {
+                published = k;
+                lds_st(ctl + C_LOADED + j, k);
             }
             if (lds_ld(ctl + C_ABORT) || lds_ld(ctl + C_DONE)) break;
             if (clk() - t0 > TIMEOUT_TICKS) {
@@ -686,8 +719,10 @@ __device__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& l
             continue;
         }
         t0 = clk();
+        unsigned gpos = (b * BATCH) % SB;
+        unsigned rpos = (b * BATCH) % RB;
 #pragma unroll
-        for (int k = 0; k < LB; ++k) {
+        for (int u = 0; u < LB; ++u) {
             unsigned lo = gpos + (unsigned)lane * 16u;
             if (lo >= SB) lo -= SB;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + lo),
@@ -696,33 +731,54 @@ __device__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& l
             gpos += 1024u;
             if (gpos >= SB) gpos -= SB;
             rpos += 1024u;
-            if (rpos >= RB) rpos -= RB;
         }
-        u += LB;
-        if (u >= (unsigned)INFL) {
-            asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // INFL - LB units may stay in flight
-            const unsigned done = u - (INFL - LB);
+        ++k;
+        if (k * LB >= (unsigned)INFL) {
+            asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // INFL - LB units may stay in flight
+            const unsigned done = k - (INFL - LB) / LB;
             if (done > published) {
                 published = done;
-                lds_st(ctl + C_LOADED, done * 64u);
+                lds_st(ctl + C_LOADED + j, done);
             }
         }
     }
     drain();
-    lds_st(ctl + C_LOADED, u * 64u);
+    lds_st(ctl + C_LOADED + j, k);
 }
 
 // ------------------------------------------------------------------ compute waves
 typedef __attribute__((ext_vector_type(4))) short bf16x4_t;
 
+// bytes of the stream landed in the ring: the prefix every loader wave has completed (wave j
+// completed its first k_j batches = global batches j, j + NL, ...: batch b = j + NL m is in iff m < k_j)
+__device__ __forceinline__ unsigned loaded_bytes(unsigned* ctl) {
+    unsigned p = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        const unsigned b = (unsigned)j + NL * lds_ld(ctl + C_LOADED + j);
+        p = b < p ? b : p;
+    }
+    return p * BATCH;
+}
 // wait until the stream bytes [.., end) are in the ring
 __device__ __forceinline__ bool wait_loaded(unsigned* ctl, unsigned end, const Args& a, int s) {
-    return lds_wait_ge(ctl, C_LOADED, (end + 15u) >> 4, a, 50, s);
+    if (loaded_bytes(ctl) >= end) return true;
+    const u64 t0 = clk();
+    for (;;) {
+        if (loaded_bytes(ctl) >= end) return true;
+        if (lds_ld(ctl + C_ABORT)) return false;
+        if (clk() - t0 > TIMEOUT_TICKS) {
+            set_err(a, E_WAIT_LDS, 50, s);
+            lds_st(ctl + C_ABORT, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 // profiling variant: adds the ticks spent waiting for the ring to *acc
 __device__ __forceinline__ bool wait_loaded_t(unsigned* ctl, unsigned end, const Args& a, int s, u64* acc,
                                               bool tracing) {
-    if (!tracing || lds_ld(ctl + C_LOADED) >= ((end + 15u) >> 4)) return wait_loaded(ctl, end, a, s);
+    if (!tracing || loaded_bytes(ctl) >= end) return wait_loaded(ctl, end, a, s);
     const u64 t0 = wall_clock64();
     const bool ok = wait_loaded(ctl, end, a, s);
     *acc += wall_clock64() - t0;
@@ -1171,13 +1227,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void dataflow_decode_kernel(Args a) {
     __syncthreads();  // the only workgroup barrier: control words zeroed before any role starts
     if (wave == 0) {
         comm_wave<D, R>(a, cu, smem, ly, lane);
-    } else if (wave == 1) {
+    } else if (wave <= NL) {
         if (a.nt_weights)
-            loader_wave<true>(a, cu, smem, ly, lane);
+            loader_wave<true>(a, cu, smem, ly, wave - 1, lane);
         else
-            loader_wave<false>(a, cu, smem, ly, lane);
+            loader_wave<false>(a, cu, smem, ly, wave - 1, lane);
     } else {
-        compute_wave<D, R, PFG>(a, cu, smem, ly, wave - 2, lane);
+        compute_wave<D, R, PFG>(a, cu, smem, ly, wave - 1 - NL, lane);
     }
 }
 
@@ -1191,6 +1247,7 @@ extern "C" int dlms_df_layer_size() { return (int)sizeof(df::Layer); }
 extern "C" int dlms_df_lds_fixed(int D, int R, int max_nq, int swl) { return df::lds_layout(D, R, max_nq, swl, 0).total; }
 extern "C" long long dlms_df_step_words(int R, int D, int L, int C) { return df::scratch_layout(R, D, L, C).words; }
 extern "C" int dlms_df_threads() { return df::NTHREADS; }
+extern "C" int dlms_df_copies() { return df::COPIES; }
 
 template <int D, int R, int PFG>
 static hipError_t df_launch(const df::Args& a, int grid, int lds, hipStream_t stream) {
@@ -1209,7 +1266,7 @@ static hipError_t df_launch(const df::Args& a, int grid, int lds, hipStream_t st
 extern "C" int dlms_dataflow_decode(const df::Args* args, int grid, hipStream_t stream) {
     const df::Args& a = *args;
     const int lds = df::lds_layout(a.D, a.R, a.max_nq, a.swl, a.ring_bytes).total;
-    if (lds > df::LDS_MAX || a.ring_bytes % (df::LB * 1024) || a.ring_bytes < 8 * 1024 || grid <= 0 || a.R < 1 || a.R > 2 ||
+    if (lds > df::LDS_MAX || a.ring_bytes % df::BATCH || a.ring_bytes < 8 * 1024 || grid <= 0 || a.R < 1 || a.R > 2 ||
         a.H * 64 != a.D || a.max_nq > 64 || a.ko % 16 || a.kf % 16 || a.ko > 64 || a.kf > 64 || a.kf < 16 || a.nsteps <= 0 || a.C != df::COPIES || a.A < 1 || a.A > grid)
         return (int)hipErrorInvalidValue;
 #define DF_CASE(DD)                                                                           \

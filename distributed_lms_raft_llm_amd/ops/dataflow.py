@@ -64,7 +64,7 @@ def _bind_once():
         return L
     L.dlms_dataflow_decode.argtypes = [ctypes.POINTER(DfArgs), ctypes.c_int, P]
     L.dlms_dataflow_decode.restype = ctypes.c_int
-    for n in ("dlms_df_args_size", "dlms_df_cu_size", "dlms_df_layer_size", "dlms_df_threads"):
+    for n in ("dlms_df_args_size", "dlms_df_cu_size", "dlms_df_layer_size", "dlms_df_threads", "dlms_df_copies"):
         getattr(L, n).restype = ctypes.c_int
     L.dlms_df_lds_fixed.argtypes = [ctypes.c_int] * 4
     L.dlms_df_lds_fixed.restype = ctypes.c_int
@@ -181,7 +181,6 @@ def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]
 class DataflowDecoder:
     """Persistent dataflow decode bound to one ``HipGPT2Engine`` (TP=1, bf16, 1-2 rows)."""
 
-    COPIES = 2  # fixed-point residual copies (workgroup c adds into copy c % COPIES)
 
     @staticmethod
     def supported(eng) -> bool:
@@ -193,6 +192,7 @@ class DataflowDecoder:
         if not self.supported(eng):
             raise ValueError("dataflow decode: TP=1 bf16 GPT-2 with d in %s only" % (SUPPORTED_D,))
         self.L = _bind_once()
+        self.COPIES = int(self.L.dlms_df_copies())  # fixed-point residual copies (CU c adds into copy c % COPIES)
         self.eng = eng
         cfg, dev = eng.cfg, eng.device
         props = torch.cuda.get_device_properties(dev)
