@@ -54,8 +54,28 @@ def spawn_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    return next((rc for rc in rcs if rc), 0)
+    # poll all ranks: if one dies, the others may block forever in a collective, so terminate
+    # (then kill) the rest and return the failing rank's code instead of hanging
+    import time
+
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = next((rc for rc in rcs if rc not in (None, 0)), None)
+        if bad is not None:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 10
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 def latency_point(eng, cfg, B: int, prompt_len: int, max_length: int, reps: int, seed: int, gpu: bool) -> dict:
@@ -192,7 +212,7 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC,
-            "value": round(tok_s, 1),
+            "value": round(tok_s, 1) if tok_s >= 100 else round(tok_s, 4),  # (CPU contract runs: < 1 tok/s)
             "unit": "tokens/s",
             "n_gpus": world if gpu else 0,
             "steps": args.steps,

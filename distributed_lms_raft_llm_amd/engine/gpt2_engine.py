@@ -477,8 +477,12 @@ class HipGPT2Engine:
         elif r.M * self.w.n_heads_local <= self.SPLIT_ATTN_MAX_PAIRS:
             # decode with few (row, head) pairs: split-K flash-decode puts NW waves on each pair's keys
             nw, ns = ops.attention_split_geometry(r.M * self.w.n_heads_local, self.max_length)
+            if r.part:
+                # concurrent row parts (multi-stream small step) would share the one workspace's
+                # partials and arrival counters: keep each (row, head) pair in one workgroup
+                ns = 1
             ops.attention_split(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
-                                waves=nw, splits=ns, workspace=self.attn_ws)
+                                waves=nw, splits=ns, workspace=self.attn_ws if ns > 1 else None)
         elif r.persist_attn:
             # overlapped step: a fixed low-occupancy grid leaves wave slots to the other half's GEMMs
             ops.row_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,

@@ -113,6 +113,11 @@ class ContinuousBatcher:
             self._cv.notify()
         return fut
 
+    @property
+    def failed(self) -> BaseException | None:
+        """The error that stopped the batcher (None while it serves)."""
+        return self._error
+
     def generate(self, prompts: list[list[int]], timeout: float | None = None) -> list[list[int]]:
         futs = [self.submit(p) for p in prompts]
         return [f.result(timeout) for f in futs]
@@ -136,6 +141,10 @@ class ContinuousBatcher:
             with torch.no_grad():
                 self._loop()
         except BaseException as e:  # fail every waiter loudly instead of hanging them
+            # (the engine's device state is suspect after this -- e.g. a PeerStalled chunk left
+            # garbage in the KV cache and the xGMI error word set -- so the batcher does not try
+            # to continue: callers see `failed`, and the serving process exits for its supervisor
+            # to restart it fresh; tutor/server.py)
             with self._cv:
                 self._error = e
                 waiters = list(self._active.values()) + list(self._queue)

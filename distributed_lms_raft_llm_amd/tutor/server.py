@@ -128,7 +128,13 @@ class TutoringServicer:
         try:
             out = self.batcher.submit(ids).result(timeout=self.timeout)
         except Exception as e:
-            context.abort(grpc.StatusCode.INTERNAL, f"generation failed: {e}")
+            # a failed batcher (e.g. a tensor-parallel peer stalled in an xGMI collective) will not
+            # serve again in this process: UNAVAILABLE makes the LMS's TutoringClient fail over to
+            # a healthy replica (INTERNAL is not retried), and TutoringServer exits this process
+            # for its supervisor to restart
+            failed = getattr(self.batcher, "failed", None) is not None
+            code = grpc.StatusCode.UNAVAILABLE if failed else grpc.StatusCode.INTERNAL
+            context.abort(code, f"generation failed: {e}")
         return pb.QueryResponse(success=True, response=self.tok.decode(out, skip_special_tokens=True))
 
 
@@ -176,6 +182,7 @@ class TutoringServer:
                                            ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)])
         wire.register(self.server, "Tutoring", TutoringServicer(self.batcher, self.tok, max_length))
         self.engine = engine
+        self._stopping = threading.Event()
         self.server.add_generic_rpc_handlers((debug_handler(health=self._health),))
         self.port = self.server.add_insecure_port(f"{host}:{port}")
         if self.port == 0:
@@ -197,14 +204,33 @@ class TutoringServer:
             out.update(queued=b.q.qsize(), ok=b._t.is_alive())
         return out
 
-    def start(self):
+    def start(self, on_fatal=None, poll_s: float = 0.25):
+        """``on_fatal(error)``: called once if the batcher fails for good (a stalled TP peer, a
+        device error): the CLI exits the process non-zero so a supervisor starts a fresh one --
+        never a re-exec of a process that initialised the GPU."""
         self.server.start()
         log.info("tutoring server on port %d", self.port)
+        if on_fatal is not None:
+            def watch():
+                while not self._stopping.is_set():
+                    err = getattr(self.batcher, "failed", None)
+                    if err is not None:
+                        log.error("batcher failed (%s): this replica stops serving", err)
+                        METRICS.inc("tutor_fatal_total")
+                        on_fatal(err)
+                        return
+                    self._stopping.wait(poll_s)
+
+            threading.Thread(target=watch, name="tutor-fatal-watch", daemon=True).start()
         return self
 
     def stop(self):
+        self._stopping.set()
         self.server.stop(0.5).wait()
         self.batcher.stop()
+
+
+EXIT_FATAL = 75  # EX_TEMPFAIL: the supervisor restarts the replica
 
 
 def main(argv=None):
@@ -216,8 +242,9 @@ def main(argv=None):
     ap.add_argument("--vocab", default=None, help="GPT-2 vocab.json")
     ap.add_argument("--merges", default=None, help="GPT-2 merges.txt")
     ap.add_argument("--device", default=os.environ.get("DLMS_DEVICE", "auto"))
-    ap.add_argument("--max-batch", type=int, default=256,
-                    help="decode slots per engine; 0 = size from free HBM (engine/memory.py)")
+    ap.add_argument("--max-batch", type=int, default=0,
+                    help="decode slots per engine; 0 (default) = as many as free HBM holds (engine/memory.py), "
+                         "so one replica reaches the 1024-query operating point")
     ap.add_argument("--window-ms", type=float, default=2.0)
     ap.add_argument("--max-length", type=int, default=150)
     ap.add_argument("--repetition-penalty", type=float, default=1.2)
@@ -263,15 +290,25 @@ def main(argv=None):
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
-                         args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk).start()
-    print(f"Tutoring Server started on port {srv.port}", flush=True)
+                         args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk)
     done = threading.Event()
+    fatal: list = []
+
+    def on_fatal(err):
+        fatal.append(err)
+        done.set()
+
+    srv.start(on_fatal=on_fatal)
+    print(f"Tutoring Server started on port {srv.port}", flush=True)
     signal.signal(signal.SIGTERM, lambda *a: done.set())
     signal.signal(signal.SIGINT, lambda *a: done.set())
     done.wait()
     srv.stop()
     if proxy is not None:
         proxy.close()
+    if fatal:  # exit, never re-exec: a supervisor starts a fresh process on a clean device state
+        log.error("exiting with status %d after a fatal serving error", EXIT_FATAL)
+        os._exit(EXIT_FATAL)
 
 
 if __name__ == "__main__":

@@ -1,6 +1,9 @@
-"""HIP engine with tensor parallelism, functional check on ONE GPU: two ranks share cuda:0 over
-the gloo backend (RCCL refuses two ranks on one device; the 8-GPU RCCL/xGMI run is the driver's
-scaling bench).  Sharded kernels + all-reduce/all-gather must reproduce TP=1."""
+"""HIP engine with tensor parallelism, functional check on ONE GPU: 2, 4 or 8 ranks share cuda:0
+over the gloo backend or the one-shot xGMI kernels inside captured graphs (RCCL refuses two ranks
+on one device; the 8-GPU RCCL/xGMI run is the driver's scaling bench).  Sharded kernels +
+all-reduce/all-gather must reproduce TP=1 -- including BASELINE configs 4 and 5's geometries:
+GPT-2-large (d 1280, 20 heads) at TP=4 and GPT-2-XL (d 1600, 25 heads) at TP=8, whose uneven head
+split (4,3,3,3,3,3,3,3) and 832/768-column FFN shards run through every HIP kernel."""
 import os
 import socket
 
@@ -20,42 +23,53 @@ def _port():
     return p
 
 
-def _setup():
+GEOMETRIES = {
+    "tp5": dict(n_layer=3, n_embd=320, n_head=5, n_positions=256, vocab_size=5000, eos_token_id=4999),
+    "large": dict(n_layer=2, n_embd=1280, n_head=20, n_positions=256, vocab_size=5000, eos_token_id=4999),
+    "xl": dict(n_layer=2, n_embd=1600, n_head=25, n_positions=256, vocab_size=5000, eos_token_id=4999),
+}
+
+
+def _setup(geo="tp5"):
     from distributed_lms_raft_llm_amd.models.config import GPT2Config
     from distributed_lms_raft_llm_amd.models.gpt2 import init_gpt2_weights, perturb_norms_and_biases
 
-    cfg = GPT2Config("gpt2-tp5", n_layer=3, n_embd=320, n_head=5, n_positions=256, vocab_size=5000,
-                     eos_token_id=4999)
+    cfg = GPT2Config(f"gpt2-{geo}", **GEOMETRIES[geo])
     w = init_gpt2_weights(cfg, seed=21)
     perturb_norms_and_biases(w, scale=0.1)
+    for k, v in w.items():  # bf16-exact weights: the oracle sees what the kernels see
+        if v.dim() == 2:
+            w[k] = v.to(torch.bfloat16).float()
     g = torch.Generator().manual_seed(2)
     prompts = [torch.randint(0, 4999, (L,), generator=g).tolist() for L in (6, 17, 30)]
     return cfg, w, prompts
 
 
-def _worker(rank, world, port, q, p2p=False):
+def _worker(rank, world, port, q, p2p=False, geo="tp5"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
         from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
-        cfg, w, prompts = _setup()
+        cfg, w, prompts = _setup(geo)
         # p2p: one-shot xGMI kernels instead of gloo calls -- all on the GPU, so hipGraph capture works
         eng = HipGPT2Engine(cfg, w, max_batch=4, max_length=64, tp_group=dist.group.WORLD, use_graph=p2p, p2p=p2p)
         assert (eng.xgmi is not None) == p2p
         hid = eng.prefill_last_hidden(prompts).cpu()
         out = eng.generate(prompts)
-        q.put((rank, eng.w.head_range, hid.numpy(), out))
+        q.put((rank, eng.w.head_range, hid.numpy(), out, eng.w.ffn_range))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("p2p", [False, True], ids=["gloo", "xgmi-graph"])
-def test_tp2_on_one_gpu_matches_tp1(p2p):
+def _run_tp(geo, world, p2p):
+    """TP=world ranks on cuda:0 vs TP=1, both margin-checked against the fp32 oracle."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+    from distributed_lms_raft_llm_amd.engine.weights import shard_range
+    from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, teacher_forced_check
 
-    cfg, w, prompts = _setup()
+    cfg, w, prompts = _setup(geo)
     ref_eng = HipGPT2Engine(cfg, w, max_batch=4, max_length=64, use_graph=False)
     ref_hid = ref_eng.prefill_last_hidden(prompts).cpu()
     ref_out = ref_eng.generate(prompts)
@@ -64,20 +78,25 @@ def test_tp2_on_one_gpu_matches_tp1(p2p):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, p2p)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, p2p, geo)) for r in range(world)]
     [p.start() for p in procs]
-    res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda r: r[0])
-    [p.join(timeout=60) for p in procs]
+    try:
+        res = sorted([q.get(timeout=800) for _ in range(world)], key=lambda r: r[0])
+    finally:
+        [p.join(timeout=60) for p in procs]
+        for p in procs:
+            if p.is_alive():
+                p.kill()
     assert all(p.exitcode == 0 for p in procs)
-    assert [r[1] for r in res] == [(0, 3), (3, 5)]
+    assert [r[1] for r in res] == [shard_range(cfg.n_head, world, r) for r in range(world)]
+    ftiles = [shard_range(cfg.n_inner // 64, world, r) for r in range(world)]
+    assert [r[4] for r in res] == [(a * 64, b * 64) for a, b in ftiles]
     for r in res:
         cos = torch.nn.functional.cosine_similarity(torch.from_numpy(r[2]), ref_hid, dim=-1)
         assert bool((cos > 0.999).all()), cos
-        assert r[3] == res[0][3]
+        assert r[3] == res[0][3]  # every rank emits the same tokens
     # margin-aware exactness against the fp32 oracle (teacher-forced on each engine's own output):
-    # TP=2 and TP=1 must both pick the oracle's greedy token wherever it is decisive
-    from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, teacher_forced_check
-
+    # TP=world and TP=1 must both pick the oracle's greedy token wherever it is decisive
     oracle = GPT2Reference(cfg, w, device="cuda")
     for outs in (res[0][3], ref_out):
         decisive = total = 0
@@ -88,3 +107,22 @@ def test_tp2_on_one_gpu_matches_tp1(p2p):
             decisive += r["decisive"]
             total += r["positions"]
         assert decisive >= 0.7 * total, (decisive, total)
+    return res
+
+
+@pytest.mark.parametrize("geo,world,p2p", [("large", 4, False), ("large", 4, True), ("xl", 8, False),
+                                           ("xl", 8, True)],
+                         ids=["large-tp4-gloo", "large-tp4-xgmi-graph", "xl-tp8-gloo", "xl-tp8-xgmi-graph"])
+def test_tp_configs_4_and_5_geometry_on_one_gpu(geo, world, p2p):
+    """BASELINE configs 4 / 5: GPT-2-large's 20 heads over 4 ranks (5 each), GPT-2-XL's 25 heads
+    over 8 ranks (4,3,3,3,3,3,3,3) with 832/768-column FFN shards."""
+    res = _run_tp(geo, world, p2p)
+    if geo == "xl":
+        assert [b - a for a, b in (r[1] for r in res)] == [4, 3, 3, 3, 3, 3, 3, 3]
+        assert sorted({b - a for a, b in (r[4] for r in res)}) == [768, 832]
+
+
+@pytest.mark.parametrize("p2p", [False, True], ids=["gloo", "xgmi-graph"])
+def test_tp2_on_one_gpu_matches_tp1(p2p):
+    res = _run_tp("tp5", 2, p2p)
+    assert [r[1] for r in res] == [(0, 3), (3, 5)]
