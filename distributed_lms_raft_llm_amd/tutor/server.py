@@ -210,6 +210,10 @@ class TutoringServer:
         never a re-exec of a process that initialised the GPU."""
         self.server.start()
         log.info("tutoring server on port %d", self.port)
+        self._arm_fatal(on_fatal, poll_s)
+        return self
+
+    def _arm_fatal(self, on_fatal, poll_s: float):
         if on_fatal is not None:
             def watch():
                 while not self._stopping.is_set():
@@ -222,12 +226,92 @@ class TutoringServer:
                     self._stopping.wait(poll_s)
 
             threading.Thread(target=watch, name="tutor-fatal-watch", daemon=True).start()
-        return self
 
     def stop(self):
         self._stopping.set()
         self.server.stop(0.5).wait()
         self.batcher.stop()
+
+
+class AioTutoringServicer:
+    """``Tutoring.GetLLMAnswer`` as a coroutine: a query holds no thread while it decodes (the
+    threaded servicer parks one worker per query, capping a replica at ``workers`` queries in
+    flight -- far below the 1024-query operating point)."""
+
+    def __init__(self, batcher, tokenizer: GPT2BPE, timeout: float = 300.0):
+        self.batcher = batcher
+        self.tok = tokenizer
+        self.timeout = timeout
+
+    async def GetLLMAnswer(self, request, context):
+        import asyncio
+
+        ids = self.tok.encode(build_prompt(request.query))
+        try:
+            out = await asyncio.wait_for(asyncio.wrap_future(self.batcher.submit(ids)), self.timeout)
+        except Exception as e:
+            failed = getattr(self.batcher, "failed", None) is not None
+            code = grpc.StatusCode.UNAVAILABLE if failed else grpc.StatusCode.INTERNAL
+            await context.abort(code, f"generation failed: {e}")
+        return pb.QueryResponse(success=True, response=self.tok.decode(out, skip_special_tokens=True))
+
+
+class AioTutoringServer(TutoringServer):
+    """The continuous-batching tutoring server with a ``grpc.aio`` front end on its own event-loop
+    thread: thousands of queries in flight per replica (the reference's tutoring
+    server is a 10-thread synchronous gRPC server).  Same engine, batcher, health/debug RPCs,
+    fatal hook and stop() as ``TutoringServer``."""
+
+    def __init__(self, engine, port: int = 50054, host: str = "[::]", max_length: int = 150,
+                 repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None, chunk: int = 8):
+        import asyncio
+
+        from ..engine.scheduler import ContinuousBatcher
+
+        if not hasattr(engine, "admit"):
+            raise ValueError("the aio front end needs a slot engine (continuous batching)")
+        if engine.max_length != max_length:
+            raise ValueError("continuous batching: engine max_length differs from the server's")
+        self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
+        self.tok = tokenizer or GPT2BPE(eos_token_id=getattr(getattr(engine, "cfg", None), "eos_token_id", 50256))
+        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
+        self.batching = "continuous"
+        self.engine = engine
+        self._stopping = threading.Event()
+        self._loop = asyncio.new_event_loop()
+        self._thread = threading.Thread(target=self._loop.run_forever, name="tutor-aio", daemon=True)
+        self._thread.start()
+
+        async def make():
+            srv = grpc.aio.server(migration_thread_pool=futures.ThreadPoolExecutor(max_workers=4),
+                                  options=[("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
+                                           ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)])
+            wire.register(srv, "Tutoring", AioTutoringServicer(self.batcher, self.tok))
+            srv.add_generic_rpc_handlers((debug_handler(health=self._health),))
+            return srv, srv.add_insecure_port(f"{host}:{port}")
+
+        self.server, self.port = asyncio.run_coroutine_threadsafe(make(), self._loop).result(30)
+        if self.port == 0:
+            raise RuntimeError(f"could not bind {host}:{port}")
+
+    def start(self, on_fatal=None, poll_s: float = 0.25):
+        import asyncio
+
+        asyncio.run_coroutine_threadsafe(self.server.start(), self._loop).result(30)
+        log.info("tutoring server (aio) on port %d", self.port)
+        self._arm_fatal(on_fatal, poll_s)
+        return self
+
+    def stop(self):
+        import asyncio
+
+        self._stopping.set()
+        try:
+            asyncio.run_coroutine_threadsafe(self.server.stop(0.5), self._loop).result(10)
+        finally:
+            self.batcher.stop()
+            self._loop.call_soon_threadsafe(self._loop.stop)
+            self._thread.join(5)
 
 
 EXIT_FATAL = 75  # EX_TEMPFAIL: the supervisor restarts the replica
@@ -253,6 +337,8 @@ def main(argv=None):
     ap.add_argument("--tp", type=int, default=0, help="tensor-parallel degree under torchrun (default: world)")
     ap.add_argument("--batching", choices=("auto", "continuous", "window"), default="auto")
     ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
+    ap.add_argument("--frontend", choices=("aio", "threads"), default="aio",
+                    help="aio: asyncio gRPC front end (thousands of queries in flight); threads: a worker per query")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     args, _ = parse_with_config(ap, argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
@@ -289,8 +375,12 @@ def main(argv=None):
                           weight_dtype=args.weight_dtype)
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
-    srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
-                         args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk)
+    if args.frontend == "aio" and args.batching != "window" and hasattr(eng, "admit"):
+        srv = AioTutoringServer(eng, args.port, args.host, args.max_length, args.repetition_penalty, tokenizer=tok,
+                                chunk=args.chunk)
+    else:
+        srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
+                             args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk)
     done = threading.Event()
     fatal: list = []
 

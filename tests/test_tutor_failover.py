@@ -9,7 +9,7 @@ import grpc
 import pytest
 
 from distributed_lms_raft_llm_amd.lms.service import TutoringClient
-from distributed_lms_raft_llm_amd.tutor.server import TutoringServer
+from distributed_lms_raft_llm_amd.tutor.server import AioTutoringServer, TutoringServer
 from distributed_lms_raft_llm_amd.wire import pb
 from lms_harness import Cluster, KeywordGate
 
@@ -54,15 +54,19 @@ class SlotEngine:
         return SimpleNamespace(result=lambda: word)
 
 
-def _server(engine):
+def _server(engine, frontend="threads"):
     fatal = threading.Event()
-    srv = TutoringServer(engine, port=0, host="127.0.0.1", max_length=48, batching="continuous", chunk=4)
+    if frontend == "aio":
+        srv = AioTutoringServer(engine, port=0, host="127.0.0.1", max_length=48, chunk=4)
+    else:
+        srv = TutoringServer(engine, port=0, host="127.0.0.1", max_length=48, batching="continuous", chunk=4)
     srv.start(on_fatal=lambda e: fatal.set(), poll_s=0.02)
     return srv, fatal
 
 
-def test_stalled_replica_answers_unavailable_and_fires_fatal_hook():
-    srv, fatal = _server(SlotEngine(stall_after=1))
+@pytest.mark.parametrize("frontend", ["threads", "aio"])
+def test_stalled_replica_answers_unavailable_and_fires_fatal_hook(frontend):
+    srv, fatal = _server(SlotEngine(stall_after=1), frontend)
     try:
         stub = __import__("distributed_lms_raft_llm_amd.wire", fromlist=["Stub"])
         s = stub.Stub("Tutoring", stub.channel(f"127.0.0.1:{srv.port}"))
@@ -77,9 +81,10 @@ def test_stalled_replica_answers_unavailable_and_fires_fatal_hook():
         srv.stop()
 
 
-def test_lms_answers_from_the_surviving_replica(tmp_path):
-    bad, bad_fatal = _server(SlotEngine(stall_after=1))
-    good, good_fatal = _server(SlotEngine())
+@pytest.mark.parametrize("frontend", ["threads", "aio"])
+def test_lms_answers_from_the_surviving_replica(tmp_path, frontend):
+    bad, bad_fatal = _server(SlotEngine(stall_after=1), frontend)
+    good, good_fatal = _server(SlotEngine(), frontend)
     # the stalled replica first in the list: the LMS must fail over, not answer "unavailable"
     tutors = f"127.0.0.1:{bad.port},127.0.0.1:{good.port}"
     c = Cluster(3, tmp_path, tutor_address=tutors, gate=KeywordGate())
@@ -105,3 +110,21 @@ def test_client_does_not_fail_over_on_internal_errors():
     """INTERNAL (a bug, not a dead replica) still surfaces: only UNAVAILABLE / CANCELLED fail over."""
     assert grpc.StatusCode.INTERNAL not in TutoringClient.RETRY_CODES
     assert grpc.StatusCode.UNAVAILABLE in TutoringClient.RETRY_CODES
+
+
+def test_aio_frontend_serves_many_concurrent_requests():
+    """The grpc.aio front end holds every in-flight RPC as a coroutine (no thread per request):
+    256 concurrent calls through a 4-slot engine all complete."""
+    from concurrent import futures as cf
+
+    srv, fatal = _server(SlotEngine(max_batch=4), "aio")
+    try:
+        stub = __import__("distributed_lms_raft_llm_amd.wire", fromlist=["Stub"])
+        s = stub.Stub("Tutoring", stub.channel(f"127.0.0.1:{srv.port}"))
+        with cf.ThreadPoolExecutor(64) as ex:
+            outs = list(ex.map(lambda i: s.GetLLMAnswer(pb.QueryRequest(token="t", query=f"q{i}"), timeout=60),
+                               range(256)))
+        assert len(outs) == 256 and all(o.success for o in outs)
+        assert not fatal.is_set()
+    finally:
+        srv.stop()
