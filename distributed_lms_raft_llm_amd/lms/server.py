@@ -42,7 +42,7 @@ class LMSServer:
     def __init__(self, node_id: int, port: int, peers: dict[int, str], data_dir: str, host: str = "[::]",
                  advertise: str | None = None, tutor_address: str | None = None, gate=None,
                  raft_config: RaftConfig | None = None, fsync: bool = True, workers: int = 32,
-                 snapshot_every: int = 2000):
+                 snapshot_every: int = 2000, frontend: str = "aio"):
         self.id = node_id
         self.port = port
         self.peers = dict(peers)
@@ -69,14 +69,41 @@ class LMSServer:
             gate.attach_state(self.state)
         opts = [("grpc.max_send_message_length", wire.DEFAULT_MAX_MESSAGE),
                 ("grpc.max_receive_message_length", wire.DEFAULT_MAX_MESSAGE)]
-        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers), options=opts)
         self.raft_servicer = RaftServicer(self.node, self.addresses, blocked=self.transport.blocked)
-        wire.register(self.server, "LMS", self.lms)
-        wire.register(self.server, "RaftService", self.raft_servicer)
-        wire.register(self.server, "FileTransferService", FileTransferServicer(self.state))
-        self.server.add_generic_rpc_handlers((snapshot_handler(self.node), fetch_handler(self.state.blobs),
-                                              debug_handler(health=self._health, status=self._status)))
-        bound = self.server.add_insecure_port(f"{host}:{port}")
+        self.frontend = frontend
+        self._loop = None
+
+        def populate(server, lms):
+            wire.register(server, "LMS", lms)
+            wire.register(server, "RaftService", self.raft_servicer)
+            wire.register(server, "FileTransferService", FileTransferServicer(self.state))
+            server.add_generic_rpc_handlers((snapshot_handler(self.node), fetch_handler(self.state.blobs),
+                                             debug_handler(health=self._health, status=self._status)))
+            return server.add_insecure_port(f"{host}:{port}")
+
+        if frontend == "aio":
+            # grpc.aio on its own event-loop thread: the synchronous handlers (Raft RPCs, writes,
+            # reads) run on the ``workers`` pool exactly as before, while GetLLMAnswer awaits the
+            # tutoring tier on the loop, so in-flight tutoring queries are not capped by the pool
+            import asyncio
+
+            self._pool = futures.ThreadPoolExecutor(max_workers=workers, thread_name_prefix="lms")
+            self._loop = asyncio.new_event_loop()
+            self._loop.set_default_executor(self._pool)
+            self._loop_thread = threading.Thread(target=self._loop.run_forever, name=f"lms{node_id}-aio",
+                                                 daemon=True)
+            self._loop_thread.start()
+
+            async def make():
+                srv = grpc.aio.server(migration_thread_pool=self._pool, options=opts)
+                return srv, populate(srv, _AioLMSView(self.lms))
+
+            self.server, bound = asyncio.run_coroutine_threadsafe(make(), self._loop).result(30)
+        elif frontend == "threads":
+            self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers), options=opts)
+            bound = populate(self.server, self.lms)
+        else:
+            raise ValueError(f"unknown frontend {frontend!r}")
         if bound == 0:
             raise RuntimeError(f"could not bind {host}:{port}")
         self.port = bound
@@ -92,8 +119,16 @@ class LMSServer:
         st["blobs_pushed"], st["blobs_fetched"] = self.replicator.pushed, self.fetcher.fetched
         return st
 
+    def _on_loop(self, coro, timeout: float = 30.0):
+        import asyncio
+
+        return asyncio.run_coroutine_threadsafe(coro, self._loop).result(timeout)
+
     def start(self):
-        self.server.start()
+        if self._loop is not None:
+            self._on_loop(self.server.start())
+        else:
+            self.server.start()
         self.node.start()
         log.info("LMS server %d listening on %s (peers %s)", self.id, self.port, self.peers)
         return self
@@ -103,7 +138,17 @@ class LMSServer:
         self.transport.close()
         self.replicator.close()
         self.fetcher.close()
-        self.server.stop(grace).wait()
+        if self._loop is not None:
+            try:
+                self._on_loop(self.server.stop(grace))
+                if self.tutor is not None:
+                    self._on_loop(self.tutor.aclose())
+            finally:
+                self._loop.call_soon_threadsafe(self._loop.stop)
+                self._loop_thread.join(5)
+                self._pool.shutdown(wait=False)
+        else:
+            self.server.stop(grace).wait()
         self.storage.close()
         if self.tutor is not None:
             self.tutor.close()
@@ -112,6 +157,18 @@ class LMSServer:
         """Fault injection: drop all Raft traffic to/from ``peers`` (both directions)."""
         self.transport.blocked.clear()
         self.transport.blocked.update(peers)
+
+
+class _AioLMSView:
+    """The LMS servicer as the aio server sees it: GetLLMAnswer is the coroutine, every other
+    method is the synchronous one (run on the migration thread pool)."""
+
+    def __init__(self, servicer: LMSServicer):
+        self._svc = servicer
+        self.GetLLMAnswer = servicer.GetLLMAnswerAsync
+
+    def __getattr__(self, name):
+        return getattr(self._svc, name)
 
 
 def cluster_from_args(args, conf: dict) -> tuple[dict[int, str], int, str | None]:
@@ -148,6 +205,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--heartbeat", type=float, default=0.05)
     ap.add_argument("--no-fsync", action="store_true")
     ap.add_argument("--snapshot-every", type=int, default=2000)
+    ap.add_argument("--workers", type=int, default=32, help="thread pool for the synchronous RPC handlers")
+    ap.add_argument("--frontend", choices=("aio", "threads"), default="aio",
+                    help="aio: GetLLMAnswer awaits the tutoring tier without holding a worker thread")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     return ap
 
@@ -168,7 +228,8 @@ def main(argv=None):
                                     weights=args.gate_weights, vocab=args.vocab)
     srv = LMSServer(args.id, args.port, peers, args.data_dir or f"lms_node{args.id}", host=args.host,
                     advertise=args.advertise, tutor_address=args.tutor or None, gate=gate, raft_config=cfg,
-                    fsync=not args.no_fsync, snapshot_every=args.snapshot_every).start()
+                    fsync=not args.no_fsync, snapshot_every=args.snapshot_every, workers=args.workers,
+                    frontend=args.frontend).start()
     done = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: done.set())
     signal.signal(signal.SIGINT, lambda *a: done.set())

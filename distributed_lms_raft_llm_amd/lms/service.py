@@ -83,6 +83,7 @@ class TutoringClient:
         self._inflight = [0] * len(self.addresses)
         self._down_until = [0.0] * len(self.addresses)
         self._lock = threading.Lock()
+        self._aio_channels = self._aio_stubs = None
 
     def _order(self) -> list[int]:
         now = time.monotonic()
@@ -111,6 +112,36 @@ class TutoringClient:
                 with self._lock:
                     self._inflight[i] -= 1
         raise last
+
+    async def ask_async(self, token: str, query: str) -> pb.QueryResponse:
+        """``ask`` on ``grpc.aio`` channels (created on first use, on the calling event loop)."""
+        if self._aio_stubs is None:
+            self._aio_channels = [grpc.aio.insecure_channel(a, options=wire.CHANNEL_OPTIONS) for a in self.addresses]
+            self._aio_stubs = [wire.Stub("Tutoring", c) for c in self._aio_channels]
+        last = None
+        for i in self._order():
+            with self._lock:
+                self._inflight[i] += 1
+            try:
+                return await self._aio_stubs[i].GetLLMAnswer(pb.QueryRequest(token=token, query=query),
+                                                             timeout=self.timeout)
+            except grpc.RpcError as e:
+                last = e
+                if e.code() not in self.RETRY_CODES:
+                    raise
+                METRICS.inc("tutor_failover_total")
+                log.warning("tutoring replica %s unavailable, failing over", self.addresses[i])
+                with self._lock:
+                    self._down_until[i] = time.monotonic() + self.down_s
+            finally:
+                with self._lock:
+                    self._inflight[i] -= 1
+        raise last
+
+    async def aclose(self):
+        for c in self._aio_channels or ():
+            await c.close()
+        self._aio_channels = self._aio_stubs = None
 
     def close(self):
         for c in self._channels:
@@ -380,8 +411,9 @@ class LMSServicer:
         return pb.GetResponse(success=True, entries=[pb.DataEntry(id=user, data=t) for t in texts])
 
     # ------------------------------------------------------------------ LLM tutoring
-    def GetLLMAnswer(self, request, context):
-        t0 = time.perf_counter()
+    def _llm_prelude(self, request, context):
+        """Everything of GetLLMAnswer before the tutoring call (session, assignment, relevance
+        gate): a final ``QueryResponse``, or ``None`` when the query goes to the tutoring tier."""
         s = self._session(request.token)
         if s is None:
             # sessions replicate through the log; a brand-new token may not have reached this node yet
@@ -413,15 +445,45 @@ class LMSServicer:
                 return pb.QueryResponse(success=True, response=MSG_LLM_IRRELEVANT)
         if self.tutor is None:
             return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        return None
+
+    def _llm_done(self, t0: float, tt: float):
+        TRACER.complete("lms.tutor_call", tt, cat="lms")
+        TRACER.complete("lms.GetLLMAnswer", t0, cat="lms")
+        METRICS.observe("llm_answer_ms", (time.perf_counter() - t0) * 1e3)
+
+    def GetLLMAnswer(self, request, context):
+        t0 = time.perf_counter()
+        early = self._llm_prelude(request, context)
+        if early is not None:
+            return early
         tt = time.perf_counter()
         try:
             resp = self.tutor.ask(request.token, request.query)
         except grpc.RpcError as e:
             log.warning("tutoring call failed: %s", e.code())
             return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
-        TRACER.complete("lms.tutor_call", tt, cat="lms")
-        TRACER.complete("lms.GetLLMAnswer", t0, cat="lms", user=user)
-        METRICS.observe("llm_answer_ms", (time.perf_counter() - t0) * 1e3)
+        self._llm_done(t0, tt)
+        return resp
+
+    async def GetLLMAnswerAsync(self, request, context):
+        """GetLLMAnswer for the ``grpc.aio`` front end (LMSServer ``frontend="aio"``): the short
+        prelude (state reads, the batched relevance gate) runs on the server's thread pool, the
+        long tutoring call is awaited on the event loop -- a query in flight holds no thread, so
+        one LMS node carries thousands of concurrent tutoring queries."""
+        import asyncio
+
+        t0 = time.perf_counter()
+        early = await asyncio.get_running_loop().run_in_executor(None, self._llm_prelude, request, context)
+        if early is not None:
+            return early
+        tt = time.perf_counter()
+        try:
+            resp = await self.tutor.ask_async(request.token, request.query)
+        except grpc.RpcError as e:
+            log.warning("tutoring call failed: %s", e.code())
+            return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        self._llm_done(t0, tt)
         return resp
 
     def WhoIsLeader(self, request, context):
