@@ -70,7 +70,7 @@ class TutoringClient:
 
     RETRY_CODES = (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.CANCELLED)
 
-    def __init__(self, address, timeout: float = 120.0, down_s: float = 2.0):
+    def __init__(self, address, timeout: float = 120.0, down_s: float = 2.0, aio_connections: int = 4):
         addrs = address.split(",") if isinstance(address, str) else list(address)
         self.addresses = [a.strip() for a in addrs if a.strip()]
         if not self.addresses:
@@ -84,6 +84,7 @@ class TutoringClient:
         self._down_until = [0.0] * len(self.addresses)
         self._lock = threading.Lock()
         self._aio_channels = self._aio_stubs = None
+        self.aio_connections = max(1, aio_connections)
 
     def _order(self) -> list[int]:
         now = time.monotonic()
@@ -116,15 +117,21 @@ class TutoringClient:
     async def ask_async(self, token: str, query: str) -> pb.QueryResponse:
         """``ask`` on ``grpc.aio`` channels (created on first use, on the calling event loop)."""
         if self._aio_stubs is None:
-            self._aio_channels = [grpc.aio.insecure_channel(a, options=wire.CHANNEL_OPTIONS) for a in self.addresses]
-            self._aio_stubs = [wire.Stub("Tutoring", c) for c in self._aio_channels]
+            # ``aio_connections`` connections per replica (own subchannel pools): a replica's
+            # front-end processes share its port through SO_REUSEPORT, which balances connections
+            opts = list(wire.CHANNEL_OPTIONS) + [("grpc.use_local_subchannel_pool", 1)]
+            self._aio_channels = [[grpc.aio.insecure_channel(a, options=opts) for _ in range(self.aio_connections)]
+                                  for a in self.addresses]
+            self._aio_stubs = [[wire.Stub("Tutoring", c) for c in cs] for cs in self._aio_channels]
+            self._rr = 0
         last = None
         for i in self._order():
             with self._lock:
                 self._inflight[i] += 1
             try:
-                return await self._aio_stubs[i].GetLLMAnswer(pb.QueryRequest(token=token, query=query),
-                                                             timeout=self.timeout)
+                self._rr += 1
+                stub = self._aio_stubs[i][self._rr % self.aio_connections]
+                return await stub.GetLLMAnswer(pb.QueryRequest(token=token, query=query), timeout=self.timeout)
             except grpc.RpcError as e:
                 last = e
                 if e.code() not in self.RETRY_CODES:
@@ -139,8 +146,9 @@ class TutoringClient:
         raise last
 
     async def aclose(self):
-        for c in self._aio_channels or ():
-            await c.close()
+        for cs in self._aio_channels or ():
+            for c in cs:
+                await c.close()
         self._aio_channels = self._aio_stubs = None
 
     def close(self):

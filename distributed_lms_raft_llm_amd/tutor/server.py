@@ -314,6 +314,42 @@ class AioTutoringServer(TutoringServer):
             self._thread.join(5)
 
 
+class PooledTutoringServer(TutoringServer):
+    """The continuous-batching engine behind ``n`` front-end processes (``tutor/frontend.py``):
+    this process keeps the GPU and the scheduler; gRPC termination and (de)tokenization run in
+    the front ends, which share the public port.  Same health/metrics surface, fatal hook and
+    stop() as ``TutoringServer``."""
+
+    def __init__(self, engine, pool, max_length: int = 150, repetition_penalty: float = 1.2, chunk: int = 8):
+        from ..engine.scheduler import ContinuousBatcher
+
+        if not hasattr(engine, "admit"):
+            raise ValueError("the front-end pool needs a slot engine (continuous batching)")
+        if engine.max_length != max_length:
+            raise ValueError("continuous batching: engine max_length differs from the server's")
+        self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
+        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
+        self.batching = "continuous"
+        self.engine = engine
+        self.pool = pool
+        self.port = 0
+        self._stopping = threading.Event()
+
+    def start(self, on_fatal=None, poll_s: float = 0.25):
+        self.pool.serve(self.batcher, health=self._health)
+        self.port = self.pool.port
+        log.info("tutoring server on port %d (%d front-end processes)", self.port, self.pool.n)
+        self._arm_fatal(on_fatal, poll_s)
+        return self
+
+    def stop(self):
+        self._stopping.set()
+        try:
+            self.pool.stop()
+        finally:
+            self.batcher.stop()
+
+
 EXIT_FATAL = 75  # EX_TEMPFAIL: the supervisor restarts the replica
 
 
@@ -339,12 +375,25 @@ def main(argv=None):
     ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
     ap.add_argument("--frontend", choices=("aio", "threads"), default="aio",
                     help="aio: asyncio gRPC front end (thousands of queries in flight); threads: a worker per query")
+    ap.add_argument("--frontends", type=int, default=4,
+                    help="gRPC front-end processes sharing the port (tutor/frontend.py); 0 = serve gRPC in "
+                         "this process (--frontend)")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     args, _ = parse_with_config(ap, argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    tp_group = proxy = None
+    tp_group = proxy = pool = None
+    if args.frontends > 0 and args.batching != "window":
+        # spawned before anything here touches the GPU; only the rank that serves a TP group
+        # (every --tp-th rank under torchrun) gets front ends, on its group's port
+        tp = args.tp or world
+        rank = int(os.environ.get("RANK", "0"))
+        if rank % tp == 0:
+            from .frontend import FrontendPool
+
+            pool = FrontendPool(args.frontends, args.port + rank // tp, args.host, args.vocab, args.merges,
+                                eos=gpt2_config(args.model).eos_token_id)
     if world > 1:  # torchrun: TP groups of --tp consecutive ranks, one front end (port + group) each
         import torch.distributed as dist
 
@@ -375,7 +424,15 @@ def main(argv=None):
                           weight_dtype=args.weight_dtype)
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
-    if args.frontend == "aio" and args.batching != "window" and hasattr(eng, "admit"):
+    if pool is not None and hasattr(eng, "admit"):
+        srv = PooledTutoringServer(eng, pool, args.max_length, args.repetition_penalty, chunk=args.chunk)
+    else:
+        if pool is not None:  # not a slot engine (CPU window batching): serve in-process
+            pool.stop(timeout=2)
+            pool = None
+    if pool is not None:
+        pass
+    elif args.frontend == "aio" and args.batching != "window" and hasattr(eng, "admit"):
         srv = AioTutoringServer(eng, args.port, args.host, args.max_length, args.repetition_penalty, tokenizer=tok,
                                 chunk=args.chunk)
     else:

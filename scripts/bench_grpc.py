@@ -64,7 +64,10 @@ def _client_main(conn):
 
     async def run(cfg):
         rng = random.Random(cfg["seed"])
-        chans = [grpc.aio.insecure_channel(a, options=wire.CHANNEL_OPTIONS) for a in cfg["addrs"]]
+        # several connections per address (own subchannel pools): the server's front-end
+        # processes share the port through SO_REUSEPORT, which balances connections
+        opts = list(wire.CHANNEL_OPTIONS) + [("grpc.use_local_subchannel_pool", 1)]
+        chans = [grpc.aio.insecure_channel(a, options=opts) for a in cfg["addrs"] for _ in range(cfg["channels"])]
         stubs = [wire.Stub(cfg["service"], c) for c in chans]
         recs, samples = [], []
         out = {"n": 0}
@@ -78,7 +81,7 @@ def _client_main(conn):
                                                              timeout=cfg["timeout"])
                 ok, n = bool(r.success), len(r.response)
             except grpc.RpcError as e:
-                ok, n = False, -abs(e.code().value[0])
+                ok, n = False, e.code().name
             out["n"] -= 1
             recs.append((t_send, (time.time() - t_send) * 1e3, ok, n))
 
@@ -153,11 +156,17 @@ class NullSlotEngine:
         return [self.tok[s, :self.len[s]].tolist() for s in slots]
 
 
-def serve_null(port_file: str, max_batch: int, max_length: int, step_ms: float, chunk: int):
-    from distributed_lms_raft_llm_amd.tutor.server import AioTutoringServer
+def serve_null(frontends: int, max_batch: int, max_length: int, step_ms: float, chunk: int):
+    from distributed_lms_raft_llm_amd.tutor.server import AioTutoringServer, PooledTutoringServer
 
-    srv = AioTutoringServer(NullSlotEngine(max_batch, max_length, step_ms), port=0, host="127.0.0.1",
-                            max_length=max_length, chunk=chunk).start()
+    eng = NullSlotEngine(max_batch, max_length, step_ms)
+    if frontends > 0:
+        from distributed_lms_raft_llm_amd.tutor.frontend import FrontendPool
+
+        srv = PooledTutoringServer(eng, FrontendPool(frontends, 0, "127.0.0.1"), max_length=max_length,
+                                   chunk=chunk).start()
+    else:
+        srv = AioTutoringServer(eng, port=0, host="127.0.0.1", max_length=max_length, chunk=chunk).start()
     print(f"Tutoring Server started on port {srv.port}", flush=True)
     done = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: done.set())
@@ -195,11 +204,12 @@ def start_tutor(args, log):
     if args.engine == "null":
         cmd = [sys.executable, os.path.abspath(__file__), "--serve-null", "--max-length", str(args.max_length),
                "--null-slots", str(args.null_slots), "--null-step-ms", str(args.null_step_ms),
-               "--chunk", str(args.chunk)]
+               "--chunk", str(args.chunk), "--frontends", str(args.frontends)]
     else:
         cmd = [sys.executable, "-m", "distributed_lms_raft_llm_amd.tutor.server", "--port", "0", "--host",
                "127.0.0.1", "--max-length", str(args.max_length), "--chunk", str(args.chunk),
-               "--model", args.model, "--max-batch", str(args.max_batch), "--frontend", "aio"]
+               "--model", args.model, "--max-batch", str(args.max_batch), "--frontend", "aio",
+               "--frontends", str(args.frontends)]
     p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     line = _wait_line(p, "Tutoring Server started on port", args.startup_timeout, log)
     _drain(p, log)
@@ -273,9 +283,17 @@ def lms_setup(addrs, n_students, timeout):
 
 
 def metrics(addr):
+    import grpc
+
     from distributed_lms_raft_llm_amd.utils.debug_rpc import debug_call
 
-    return debug_call(addr, "Metrics", timeout=10)
+    for attempt in range(5):
+        try:
+            return debug_call(addr, "Metrics", timeout=10)
+        except grpc.RpcError:
+            if attempt == 4:
+                raise
+            time.sleep(0.05)
 
 
 def main():
@@ -285,6 +303,8 @@ def main():
     ap.add_argument("--duration", type=float, default=30.0)
     ap.add_argument("--warmup", type=float, default=8.0)
     ap.add_argument("--client-procs", type=int, default=4)
+    ap.add_argument("--channels", type=int, default=4, help="connections per client process and address")
+    ap.add_argument("--frontends", type=int, default=4, help="tutoring front-end processes (0: in-process aio)")
     ap.add_argument("--engine", choices=("hip", "null"), default="hip")
     ap.add_argument("--model", default="gpt2")
     ap.add_argument("--max-batch", type=int, default=0, help="tutor slots (0: HBM planner)")
@@ -304,7 +324,7 @@ def main():
     ap.add_argument("--serve-null", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.serve_null:
-        return serve_null("", args.null_slots, args.max_length, args.null_step_ms, args.chunk)
+        return serve_null(args.frontends, args.null_slots, args.max_length, args.null_step_ms, args.chunk)
 
     # 1. clients first: fresh interpreters, before any process here touches the GPU
     ctx = mp.get_context("spawn")
@@ -340,7 +360,7 @@ def main():
             for i, (_, conn) in enumerate(clients):
                 conn.send({"addrs": addrs, "service": service, "rate": rate / len(clients), "t_begin": t_begin,
                            "t_stop": t_stop, "calls": calls[i::len(clients)], "seed": 7919 * i + int(rate),
-                           "timeout": args.timeout})
+                           "timeout": args.timeout, "channels": args.channels})
             time.sleep(max(0.0, t_meas - time.time()))
             m0, w0 = metrics(tutor_addr), time.time()
             time.sleep(max(0.0, t_stop - time.time()))
@@ -348,6 +368,9 @@ def main():
             results = [conn.recv() for _, conn in clients]
             recs = [r for rr, _ in results for r in rr]
             win = [r for r in recs if t_meas <= r[0] < t_stop]
+            if os.environ.get("BENCH_GRPC_DUMP"):
+                with open(os.environ["BENCH_GRPC_DUMP"], "w") as f:
+                    json.dump({"t_begin": t_begin, "t_meas": t_meas, "t_stop": t_stop, "recs": recs}, f)
             ok = [r for r in win if r[2]]
             done_in_win = [r for r in recs if r[2] and t_meas <= r[0] + r[1] / 1e3 < t_stop]
             lat = [r[1] for r in ok]
@@ -370,6 +393,8 @@ def main():
                 "tok_s": round(tokens_win / (w1 - w0), 1),
                 "completed_qps": round(len(done_in_win) / args.duration, 1),
                 "sent_in_window": len(win), "ok": len(ok), "failed": len(win) - len(ok),
+                "fail_codes": {c: sum(1 for r in win if not r[2] and r[3] == c)
+                               for c in sorted({r[3] for r in win if not r[2]})},
                 "p50_ms": round(pct(lat, 0.5), 1) if lat else None, "p99_ms": round(pct(lat, 0.99), 1) if lat else None,
                 "mean_ms": round(statistics.mean(lat), 1) if lat else None,
                 "inflight_mean": round(statistics.mean(infl), 1) if infl else 0,

@@ -9,7 +9,8 @@ import grpc
 import pytest
 
 from distributed_lms_raft_llm_amd.lms.service import TutoringClient
-from distributed_lms_raft_llm_amd.tutor.server import AioTutoringServer, TutoringServer
+from distributed_lms_raft_llm_amd.tutor.frontend import FrontendPool
+from distributed_lms_raft_llm_amd.tutor.server import AioTutoringServer, PooledTutoringServer, TutoringServer
 from distributed_lms_raft_llm_amd.wire import pb
 from lms_harness import Cluster, KeywordGate
 
@@ -58,13 +59,15 @@ def _server(engine, frontend="threads"):
     fatal = threading.Event()
     if frontend == "aio":
         srv = AioTutoringServer(engine, port=0, host="127.0.0.1", max_length=48, chunk=4)
+    elif frontend == "pool":
+        srv = PooledTutoringServer(engine, FrontendPool(2, 0, "127.0.0.1"), max_length=48, chunk=4)
     else:
         srv = TutoringServer(engine, port=0, host="127.0.0.1", max_length=48, batching="continuous", chunk=4)
     srv.start(on_fatal=lambda e: fatal.set(), poll_s=0.02)
     return srv, fatal
 
 
-@pytest.mark.parametrize("frontend", ["threads", "aio"])
+@pytest.mark.parametrize("frontend", ["threads", "aio", "pool"])
 def test_stalled_replica_answers_unavailable_and_fires_fatal_hook(frontend):
     srv, fatal = _server(SlotEngine(stall_after=1), frontend)
     try:
@@ -81,7 +84,7 @@ def test_stalled_replica_answers_unavailable_and_fires_fatal_hook(frontend):
         srv.stop()
 
 
-@pytest.mark.parametrize("frontend", ["threads", "aio"])
+@pytest.mark.parametrize("frontend", ["threads", "aio", "pool"])
 def test_lms_answers_from_the_surviving_replica(tmp_path, frontend):
     bad, bad_fatal = _server(SlotEngine(stall_after=1), frontend)
     good, good_fatal = _server(SlotEngine(), frontend)
@@ -112,19 +115,29 @@ def test_client_does_not_fail_over_on_internal_errors():
     assert grpc.StatusCode.UNAVAILABLE in TutoringClient.RETRY_CODES
 
 
-def test_aio_frontend_serves_many_concurrent_requests():
-    """The grpc.aio front end holds every in-flight RPC as a coroutine (no thread per request):
-    256 concurrent calls through a 4-slot engine all complete."""
+@pytest.mark.parametrize("frontend", ["aio", "pool"])
+def test_aio_frontend_serves_many_concurrent_requests(frontend):
+    """The grpc.aio front ends hold every in-flight RPC as a coroutine (no thread per request):
+    256 concurrent calls through a 4-slot engine all complete, over several connections (the
+    pool's front-end processes share the port)."""
     from concurrent import futures as cf
 
-    srv, fatal = _server(SlotEngine(max_batch=4), "aio")
+    srv, fatal = _server(SlotEngine(max_batch=4), frontend)
     try:
-        stub = __import__("distributed_lms_raft_llm_amd.wire", fromlist=["Stub"])
-        s = stub.Stub("Tutoring", stub.channel(f"127.0.0.1:{srv.port}"))
+        from distributed_lms_raft_llm_amd import wire
+        from distributed_lms_raft_llm_amd.utils.debug_rpc import debug_call
+
+        opts = list(wire.CHANNEL_OPTIONS) + [("grpc.use_local_subchannel_pool", 1)]
+        stubs = [wire.Stub("Tutoring", grpc.insecure_channel(f"127.0.0.1:{srv.port}", options=opts))
+                 for _ in range(4)]
         with cf.ThreadPoolExecutor(64) as ex:
-            outs = list(ex.map(lambda i: s.GetLLMAnswer(pb.QueryRequest(token="t", query=f"q{i}"), timeout=60),
-                               range(256)))
-        assert len(outs) == 256 and all(o.success for o in outs)
+            outs = list(ex.map(lambda i: stubs[i % 4].GetLLMAnswer(pb.QueryRequest(token="t", query=f"q{i}"),
+                                                                    timeout=60), range(256)))
+        assert len(outs) == 256 and all(o.success and o.response for o in outs)
         assert not fatal.is_set()
+        # the debug Metrics RPC reports the ENGINE's counters, whichever process answers it
+        m = debug_call(f"127.0.0.1:{srv.port}", "Metrics")
+        assert m["counters"].get("tutor_tokens", 0) > 0
+        assert debug_call(f"127.0.0.1:{srv.port}", "Health")["ok"]
     finally:
         srv.stop()
