@@ -689,7 +689,8 @@ class HipGPT2Engine:
     def _df_ok(self, B: int) -> bool:
         from ..ops.dataflow import MAX_ROWS
 
-        return self.dataflow and 1 <= B <= min(MAX_ROWS, self.max_batch)
+        # (the launch-per-op path serves row counts whose stream window outgrows the LDS ring)
+        return self.dataflow and 1 <= B <= min(MAX_ROWS, self.max_batch) and self._df_decoder().fits(B)
 
     def _df_decoder(self):
         if self._df is None:

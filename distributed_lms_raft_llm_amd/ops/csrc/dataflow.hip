@@ -130,7 +130,7 @@ __host__ __device__ inline Lay lds_layout(int D, int R, int max_nq, int swl, int
     o.mrg = off; off = align16(off + NC * R * 68 * 4);
     o.seen = off; off = align16(off + R * swl * 4);
     o.keys = off; off = align16(off + NC * R * 8);
-    o.hb = off; off = align16(off + NC * 16 * 64 * 2);                   // per-wave A staging (bf16 [16][64])
+    o.hb = off; off = align16(off + NC * R * 64 * 2);                    // per-wave A staging (bf16 [R][64])
     o.fcp = off; off = align16(off + NC * R * 64 * 4);                   // K-split c_fc partials
     o.total = off;
     return o;
@@ -859,7 +859,7 @@ __device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsig
     }
 }
 
-// A fragments of a bf16 vector staged in this wave's LDS slot hb[16][64] (row m = lane & 15; rows
+// A fragments of a bf16 vector staged in this wave's LDS slot hb[R][64] (row m = lane & 15; rows
 // m >= R and k >= nvalid are zero): fragment kb holds k = 16 kb + 4 (lane >> 4) .. + 4, read at hb
 // column k0 + k
 template <int KB, int R>
@@ -922,7 +922,7 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
     float* mrg = reinterpret_cast<float*>(lds + ly.mrg);
     const unsigned* seen = reinterpret_cast<const unsigned*>(lds + ly.seen);
     u64* keys = reinterpret_cast<u64*>(lds + ly.keys);
-    bf16_t* hb = reinterpret_cast<bf16_t*>(lds + ly.hb) + w * 16 * 64;
+    bf16_t* hb = reinterpret_cast<bf16_t*>(lds + ly.hb) + w * R * 64;
     const char* ring = lds + ly.ring;
     // every argument the loops touch, read once (kernel-argument reloads inside the loops cost a
     // scalar round trip each under SGPR pressure)

@@ -178,6 +178,16 @@ def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]
     return packed, starts
 
 
+def ring_window(cus: list[CuPlan], d: int, ko: int, kf: int, nc: int = 4) -> int:
+    """``DataflowDecoder.ring_window`` for a plan (bytes)."""
+    rowb = 2 * d + 32
+    need = 0
+    for cu in cus:
+        need = max(need, cu.nq * rowb, d * ko * 2 if cu.nk else 0, cu.nf * rowb + d * kf * 2,
+                   min(cu.nv, nc * 16) * rowb)
+    return need
+
+
 class DataflowDecoder:
     """Persistent dataflow decode bound to one ``HipGPT2Engine`` (TP=1, bf16, 1-2 rows)."""
 
@@ -233,6 +243,21 @@ class DataflowDecoder:
         fixed = self.L.dlms_df_lds_fixed(self.eng.cfg.n_embd, R, self.max_nq, self.swl)
         return (LDS_MAX - fixed) // 8192 * 8192  # a multiple of the loader's 8 KiB batches
 
+    NC = 4          # compute waves per CU (dataflow.hip NC)
+    BATCH = 8192    # loader batch bytes (dataflow.hip BATCH)
+
+    def ring_window(self) -> int:
+        """The most stream bytes a compute wave needs resident beyond the slowest wave's released
+        prefix (every wait in dataflow.hip's compute_wave): the QKV rows; the W_o block; the c_fc
+        rows + the c_proj block (consumed together); and, for the LM head's 16-row groups dealt
+        round-robin to the NC waves, NC groups.  The loader only fetches whole 8 KiB batches that
+        fit behind that prefix, so a launch needs ``ring_window() + BATCH <= ring_bytes`` or a wave
+        would wait forever for bytes the loader may not fetch (caught as a hand-off timeout)."""
+        return ring_window(self.cus, self.eng.cfg.n_embd, self.ko, self.kf, self.NC)
+
+    def fits(self, R: int) -> bool:
+        return self.ring_window() + self.BATCH <= self.ring_bytes(R)
+
     def step_words(self, R: int) -> int:
         return int(self.L.dlms_df_step_words(R, self.eng.cfg.n_embd, self.eng.cfg.n_layer, self.COPIES))
 
@@ -260,6 +285,9 @@ class DataflowDecoder:
         eng, cfg = self.eng, self.eng.cfg
         if not 1 <= B <= MAX_ROWS or nsteps <= 0:
             raise ValueError(f"dataflow run: B in [1, {MAX_ROWS}], nsteps > 0")
+        if not self.fits(B):
+            raise ValueError(f"dataflow run: a {self.ring_window()} B stream window does not fit the "
+                             f"{self.ring_bytes(B)} B ring at {B} rows (grid {self.G})")
         if nsteps * self.max_step_bytes >= 2 ** 32 - 2 ** 24:
             raise ValueError("dataflow run: too many steps for one launch (32-bit stream offsets)")
         scratch = self._scratch_for(B, nsteps)

@@ -137,3 +137,24 @@ def test_split_reproduces_the_reference_step():
     kv = [(cache.data[l, 0, 0, :, :3], cache.data[l, 1, 0, :, :3]) for l in range(cfg.n_layer)]
     got = _emulate_step(cfg, w, cus, seq[3], 3, kv)
     torch.testing.assert_close(got, hid[-1].double(), atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("name,G,window", [
+    ("gpt2", 256, 4 * 16 * 1568),            # the LM head's NC in-flight 16-row groups
+    ("gpt2-medium", 256, 4 * 16 * 2080),     # 133 KiB: fits the 144 KiB ring at 1 row only
+    ("gpt2-medium", 128, 4 * 16 * 2080),     # ... and its c_fc rows + c_proj block need 132096 B
+])
+def test_ring_window(name, G, window):
+    """The stream window a compute wave needs resident (ops/dataflow.py ring_window): the
+    gpt2-medium launches that stalled on the GPU (profiles/r3_df_hang_probe.jsonl) are exactly
+    those whose window + one 8 KiB loader batch exceeds the ring."""
+    from distributed_lms_raft_llm_amd.ops.dataflow import ring_window
+
+    cfg = gpt2_config(name)
+    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, 4)
+    ko, kf = block_k(cus)
+    assert ring_window(cus, cfg.n_embd, ko, kf) == window
+    if G == 128:  # the r3 loader stall at layer 4: the MLP window alone overflows the old ring
+        assert max(cu.nf for cu in cus) * 2080 + cfg.n_embd * kf * 2 + 8192 > 139264
+    # the r3 probe: medium at 256 CUs with the old 139264 B ring (hb staged 16 rows) stalls
+    assert ring_window(cus, cfg.n_embd, ko, kf) + 8192 > 139264 or name == "gpt2"
