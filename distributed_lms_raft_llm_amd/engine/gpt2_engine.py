@@ -293,8 +293,10 @@ class HipGPT2Engine:
         # batch 1 (TP=1, head-grouped attention): LN2 -> c_fc -> GELU -> c_proj as ONE kernel whose
         # workgroups add their 16-column slices into an int64 fixed-point residual (order-independent
         # integer atomics; ops.skinny_mlp) -- one launch and one dependent round trip fewer per layer
-        self.fused_mlp = (self.ao_groups > 0 and cfg.n_embd in (768, 1024) and self.w.ffn_local == 4 * cfg.n_embd and
-                          os.environ.get("DLMS_FUSED_MLP", "1") != "0")
+        # (any width the kernel takes: batch 1 without head groups -- GPT-2-large/XL's 20 / 25 heads --
+        # runs split attention + the in-place out-projection into the fixed-point residual first)
+        self.fused_mlp = (self.small_inplace and cfg.n_embd in ops.SKINNY_MLP_WIDTHS and
+                          self.w.ffn_local == 4 * cfg.n_embd and os.environ.get("DLMS_FUSED_MLP", "1") != "0")
         # ... and up to this many rows (2-8: split attention + in-place out-projection into the
         # fixed-point residual; each row adds 6 KB of atomics per MLP workgroup)
         self.fused_mlp_rows = int(os.environ.get("DLMS_FUSED_MLP_ROWS", "2")) if self.fused_mlp else 0
@@ -792,8 +794,8 @@ class HipGPT2Engine:
     def _decode_layers_fused_mlp(self, r, B: int):
         """Layers as [LN1 + QKV (+ clear the MLP's accumulator)] -> attention + out-projection ->
         [add + LN2 + c_fc + GELU + c_proj, added into the int64 fixed-point residual xr[l % 2]].
-        Batch 1: attention fused with the out-projection (4 head-group slabs the MLP sums); 2 or more
-        rows: split attention, then the skinny out-projection adding into the residual in place (the
+        Batch 1 with head groups (12 / 16 heads): attention fused with the out-projection (4 head-group
+        slabs the MLP sums); otherwise split attention, then the skinny out-projection adding into the residual in place (the
         f32 embedding rows x in layer 0, copy 0 of the fixed-point residual after that).  The final
         residual is xr[(L - 1) % 2]."""
         eps = self.cfg.layer_norm_epsilon
@@ -804,7 +806,7 @@ class HipGPT2Engine:
             ops.skinny_addln_gemm(xin, lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, bias=lw.b_qkv, q_out=r.q,
                                   k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos,
                                   zero=self.xr[li % 2])  # (all of its rows: a contiguous clear)
-            if B == 1:
+            if B == 1 and self.ao_groups:
                 ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
                                             self.ao_groups, tiles=self.ao_group_tiles)
                 ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc,

@@ -156,8 +156,9 @@ def _bind(L):
         "dlms_attention_oproj_grouped": [P, P, P, P, P, I, I, I, I, F, P, I, I, P, ctypes.c_longlong, P],
         "dlms_skinny_addln_gemm": [I, P, P, I, P, I, ctypes.c_longlong, I, P, P, P, F, P, I, I, I,
                                    ctypes.POINTER(GemmEpi), I, ctypes.c_longlong, P, I, P],
+        "dlms_skinny_mlp_cg": [I, I, I],
         "dlms_skinny_mlp": [P, I, I, ctypes.c_longlong, P, I, ctypes.c_longlong, I, P, P, P, F, P, P, P, P, P, I,
-                            ctypes.c_longlong, I, I, I, P],
+                            ctypes.c_longlong, I, I, I, I, P],
         "dlms_ln_fix": [P, I, ctypes.c_longlong, P, P, F, P, I, I, I, P],
         "dlms_fix_copies": [],
         "dlms_skinny_addln_max_rows": [I],
@@ -946,9 +947,17 @@ def fix_to_float(r: torch.Tensor) -> torch.Tensor:
     return (r.sum(0).to(torch.float64) / FIX_SCALE).to(torch.float32)
 
 
+SKINNY_MLP_WIDTHS = (768, 1024, 1280, 1600)  # GPT-2 small / medium / large / XL
+
+
+def skinny_mlp_cg(K: int, M: int, want: int = 0) -> int:
+    """Column groups per workgroup the fused MLP uses for M rows of width K (0: unsupported)."""
+    return int(lib().dlms_skinny_mlp_cg(K, M, want))
+
+
 def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tensor, b_fc, w_p_sl: torch.Tensor, b_p,
-               r_out: torch.Tensor, *, parts=None, nsplit: int = 0, res_bias=None):
-    """Fused latency-path MLP (TP=1, M <= 8 rows, d in {768, 1024}):
+               r_out: torch.Tensor, *, parts=None, nsplit: int = 0, res_bias=None, cg: int = 0):
+    """Fused latency-path MLP (TP=1, M <= 8 rows, d in SKINNY_MLP_WIDTHS):
 
         v = x_in + res_bias + sum(parts[:nsplit]);  h = bf16(gelu(bf16(LN(v)) @ W_fc.T + b_fc))
         r_out += fix(v + h @ W_p.T + b_p)
@@ -956,7 +965,8 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
     ``x_in``: f32 [M, d] or int64 fixed point [fix_copies(), M, d]; ``r_out``: int64 fixed point
     [fix_copies(), M, d], ZERO on entry (``skinny_addln_gemm(zero=...)`` clears it), must not alias
     ``x_in``.  Workgroup j adds its contribution into copy j % fix_copies() with 64-bit integer
-    atomics: the result is order-independent."""
+    atomics: the result is order-independent.  ``cg``: column groups of 16 intermediate columns
+    per workgroup (1, 2, 4; 0 = DLMS_MLP_CG or the per-width default; narrowed to what fits the LDS)."""
     xfix = x_in.dtype == torch.int64
     C = fix_copies()
     xcs = 0
@@ -980,8 +990,10 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
     if w_fc_sh.shape[1] * 32 != K or not w_fc_sh.is_contiguous() or tuple(w_p_sl.shape) != (F // 16, K, 16) or \
             not w_p_sl.is_contiguous():
         raise ValueError("skinny_mlp: weight layouts (shuffle_weight / slice_cproj) do not match x_in")
-    if M < 1 or M > 8 or K not in (768, 1024):
-        raise ValueError(f"skinny_mlp: M <= 8 rows of width 768 / 1024, got {tuple(x_in.shape)}")
+    if M < 1 or M > 8 or K not in SKINNY_MLP_WIDTHS:
+        raise ValueError(f"skinny_mlp: M <= 8 rows of width {SKINNY_MLP_WIDTHS}, got {tuple(x_in.shape)}")
+    if skinny_mlp_cg(K, M, cg) == 0:
+        raise ValueError(f"skinny_mlp: {M} rows of width {K} do not fit the kernel's LDS")
     if r_out.shape[0] < M or r_out.shape[1] < K or r_out.stride(1) != 1 or r_out.data_ptr() == x_in.data_ptr():
         raise ValueError("skinny_mlp: r_out too small or aliases x_in")
     if x_in.stride(1) != 1 or x_in.stride(0) % 4 or x_in.data_ptr() % 16:
@@ -990,8 +1002,8 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
         _req(t, torch.float32, n, 1)
         if t.numel() != size:
             raise ValueError(f"skinny_mlp: {n} size")
-    if nsplit not in (0, 4):
-        raise ValueError("skinny_mlp: nsplit in {0, 4}")
+    if nsplit not in (0, 4) or (nsplit and K > 1024):
+        raise ValueError("skinny_mlp: nsplit in {0, 4} (4: d <= 1024)")
     ldp, sstride = 0, 0
     if nsplit:
         _req(parts, torch.float32, "parts", 3)
@@ -1005,7 +1017,7 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
             raise ValueError("res_bias size")
     _check(lib().dlms_skinny_mlp(_p(x_in), x_in.stride(0), int(xfix), xcs, _p(parts) if nsplit else None, ldp,
                                  sstride, nsplit, _p(res_bias), _p(gamma), _p(beta), float(eps), _p(w_fc_sh), _p(b_fc),
-                                 _p(w_p_sl), _p(b_p), _p(r_out), r_out.stride(0), rcs, M, K, F, _stream()),
+                                 _p(w_p_sl), _p(b_p), _p(r_out), r_out.stride(0), rcs, M, K, F, int(cg), _stream()),
            "dlms_skinny_mlp")
     return r_full
 

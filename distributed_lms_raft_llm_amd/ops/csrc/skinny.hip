@@ -663,6 +663,8 @@ extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const void* x_in, float* x
         switch ((K / 4 + 63) / 64) {
             case 3: return addln_rpw<SK_QKV, 0, 3, true>(a, *ep, stream);
             case 4: return addln_rpw<SK_QKV, 0, 4, true>(a, *ep, stream);
+            case 5: return addln_rpw<SK_QKV, 0, 5, true>(a, *ep, stream);
+            case 7: return addln_rpw<SK_QKV, 0, 7, true>(a, *ep, stream);
             default: return hipErrorInvalidValue;
         }
     }
@@ -703,159 +705,254 @@ extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const void* x_in, float* x
 typedef __attribute__((address_space(3))) void sk_lds_void_t;
 typedef __attribute__((address_space(1))) void sk_glob_void_t;
 
-template <int NSPLIT, int NV4, int RPW, int KBW, int NC, bool XFIX>
+// CG column groups per workgroup (r3): the c_proj atomics per workgroup are M * d whatever its
+// width, so a workgroup owning CG groups divides the same-address atomic depth (F / 16 / COPIES
+// adds per residual word at CG = 1) by CG -- the atomics, not the weight stream, bounded the
+// CG = 1 kernel (profiles/r3_fused_mlp_cg.jsonl).  The NW / CG waves of a column group split its
+// K; the LayerNorm image holds only the 4 RPW rows a launch may carry.
+__host__ __device__ constexpr int mlp_img_bytes(int RPW, int NKB) {
+    return ((4 * RPW * (NKB * 64 + 16) + 1023) & ~1023) > 4096 ? ((4 * RPW * (NKB * 64 + 16) + 1023) & ~1023) : 4096;
+}
+__host__ __device__ constexpr int mlp_dyn_lds(int RPW, int NKB, int CG) {
+    return mlp_img_bytes(RPW, NKB) + CG * NKB * 1024 + 4 * RPW * NKB * 32 * 4;
+}
+__host__ __device__ constexpr bool mlp_fits(int RPW, int NKB, int CG) {
+    return mlp_dyn_lds(RPW, NKB, CG) + 16 * 16 * CG * 4 <= 160 * 1024;
+}
+
+template <int NSPLIT, int NV4, int RPW, int NKB, int CG, bool XFIX>
 __global__ __launch_bounds__(256) void skinny_mlp_kernel(
     const void* __restrict__ x_in, int ldx, const float* __restrict__ parts, int ldp, long long split_stride,
     const float* __restrict__ res_bias, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     const bf16_t* __restrict__ Wfc_sh, const float* __restrict__ b_fc, const bf16_t* __restrict__ Wp_sl,
-    const float* __restrict__ b_p, unsigned long long* __restrict__ r_out, int ldr, long long rcs, long long xcs, int M,
-    int K) {
+    const float* __restrict__ b_p, unsigned long long* __restrict__ r_out, int ldr, long long rcs, long long xcs, int M) {
     constexpr int NW = 4;
+    constexpr int K = NKB * 32;
+    constexpr int WPG = NW / CG;                // waves per column group: they split its K
+    static_assert(NW % CG == 0, "whole waves per column group");
+    constexpr int PER = (NKB + WPG - 1) / WPG;  // k-blocks per wave
+    constexpr int ROWB = K * 2 + 16;            // padded LN image rows: conflict-free fragment reads
+    constexpr int ROWS = 4 * RPW;
+    constexpr int IMG = mlp_img_bytes(RPW, NKB);
+    constexpr int WPB = CG * K * 32;            // the workgroup's W_p slices [CG][K][16] bf16
+    constexpr int PIECES = WPB / 1024;
+    constexpr int PPW = (PIECES + NW - 1) / NW;
+    constexpr int NCP = (K + 255) / 256;        // c_proj output columns per thread
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float hs[16][16];
+    __shared__ float hs[16][16 * CG];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int ng = blockIdx.x;
-    const int nkb = K >> 5;
-    const int per = (nkb + NW - 1) / NW;
-    const int kb0 = wave * per < nkb ? wave * per : nkb;
-    const int nk = (kb0 + per < nkb ? kb0 + per : nkb) - kb0;
+    const int cgi = wave / WPG;
+    const int kpart = wave % WPG;
+    const int ng = blockIdx.x * CG + cgi;       // this wave's column group (16 intermediate columns)
+    const int kb0 = kpart * PER < NKB ? kpart * PER : NKB;
+    const int nk = (kb0 + PER < NKB ? kb0 + PER : NKB) - kb0;
     const int kbl = nk > 0 ? kb0 : 0;
     const int last = nk > 0 ? nk - 1 : 0;
     const int g = lane >> 4, fr = lane & 15;
-    const int row_bytes = K * 2 + 16;
 
-    // (0) weights first: W_fc B fragments into registers; the workgroup's contiguous W_p slice
-    //     (K * 32 B) straight into LDS by LDS-DMA (no staging registers, lands under the LayerNorm);
-    //     the c_proj bias for this thread's output columns
-    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wfc_sh) + ((size_t)ng * nkb + kbl) * 64 + lane;
-    bf16x8_t b[KBW];
+    // (0) weights first: W_fc B fragments into registers; the workgroup's contiguous W_p slices
+    //     (CG * K * 32 B) straight into LDS by LDS-DMA (no staging registers, lands under the
+    //     LayerNorm); the c_proj bias for this thread's output columns
+    const bf16x8_t* wsrc = reinterpret_cast<const bf16x8_t*>(Wfc_sh) + ((size_t)ng * NKB + kbl) * 64 + lane;
+    bf16x8_t b[PER];
 #pragma unroll
-    for (int u = 0; u < KBW; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
-    const int img_bytes = (16 * row_bytes + 1023) & ~1023;
-    char* wp_lds = smem + img_bytes;                       // [K][16] bf16
-    float* v_lds = reinterpret_cast<float*>(wp_lds + K * 32);  // block 0: [M][K] f32 residual rows
-    // K = 256 NC: K * 32 B = 8 NC KiB-pieces, 2 NC per wave (a compile-time count, so the LayerNorm's
-    // wait for the activation loads issued before them is a counted vmcnt, not a drain)
-    const char* wp_src = reinterpret_cast<const char*>(Wp_sl + (size_t)ng * K * 16) + lane * 16;
+    for (int u = 0; u < PER; ++u) b[u] = load_wfrag(wsrc + (size_t)(u < nk ? u : last) * 64);
+    char* wp_lds = smem + IMG;
+    float* v_lds = reinterpret_cast<float*>(wp_lds + WPB);  // block 0: [M][K] f32 residual rows
+    const char* wp_src = reinterpret_cast<const char*>(Wp_sl + (size_t)blockIdx.x * CG * K * 16) + lane * 16;
     auto issue_wp = [&]() {
 #pragma unroll
-        for (int q = 0; q < 2 * NC; ++q) {
+        for (int q = 0; q < PPW; ++q) {
             const int pc = wave + NW * q;
-            __builtin_amdgcn_global_load_lds((sk_glob_void_t*)(wp_src + pc * 1024), (sk_lds_void_t*)(wp_lds + pc * 1024),
-                                             16, 0, 0);
+            if (PIECES % NW == 0 || pc < PIECES)
+                __builtin_amdgcn_global_load_lds((sk_glob_void_t*)(wp_src + pc * 1024),
+                                                 (sk_lds_void_t*)(wp_lds + pc * 1024), 16, 0, 0);
         }
     };
-    float bp[NC];
+    float bp[NCP];
 #pragma unroll
-    for (int i = 0; i < NC; ++i) {
+    for (int i = 0; i < NCP; ++i) {
         const int n = tid + 256 * i;
         bp[i] = (blockIdx.x == 0 && n < K) ? b_p[n] : 0.f;
     }
 
     // (1) residual rows -> LN2 -> LDS image (block 0 also keeps v); (2) c_fc slice on MFMA
     addln_rows_lds<NSPLIT, NV4, RPW, XFIX>(x_in, nullptr, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, M,
-                                           K, smem, row_bytes, xcs, blockIdx.x == 0 ? v_lds : nullptr, issue_wp);
+                                           K, smem, ROWB, xcs, blockIdx.x == 0 ? v_lds : nullptr, issue_wp);
     __syncthreads();
     f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int arow = fr < ROWS ? fr : ROWS - 1;  // rows >= M: garbage results, never stored
 #pragma unroll
-    for (int u = 0; u < KBW; ++u) {
+    for (int u = 0; u < PER; ++u) {
         if (u >= nk) continue;
-        const bf16x8_t av = lds_a_frag(smem, row_bytes, fr, kb0 + u, g);
+        const bf16x8_t av = lds_a_frag(smem, ROWB, arow, kb0 + u, g);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b[u], acc, 0, 0, 0);
     }
     __syncthreads();  // LN image no longer read: reuse it for the fixed-order K-slice reduction
     float* red = reinterpret_cast<float*>(smem);
-    if (wave > 0) *reinterpret_cast<f32x4_t*>(red + ((size_t)wave * 64 + lane) * 4) = acc;
+    if (kpart > 0) *reinterpret_cast<f32x4_t*>(red + ((size_t)wave * 64 + lane) * 4) = acc;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the W_p DMA has landed ...
     __syncthreads();                                  // ... and every other wave's
-    if (wave == 0) {
+    if (kpart == 0) {
 #pragma unroll
-        for (int s = 1; s < NW; ++s) acc += *reinterpret_cast<const f32x4_t*>(red + ((size_t)s * 64 + lane) * 4);
+        for (int s = 1; s < WPG; ++s) acc += *reinterpret_cast<const f32x4_t*>(red + ((size_t)(wave + s) * 64 + lane) * 4);
         const float bb = b_fc[ng * 16 + fr];
 #pragma unroll
         for (int r = 0; r < 4; ++r)  // bf16 rounding: the same operand the unfused c_proj reads
-            hs[g * 4 + r][fr] = bf16_to_f32(f32_to_bf16(gelu_tanh(acc[r] + bb)));
+            hs[g * 4 + r][cgi * 16 + fr] = bf16_to_f32(f32_to_bf16(gelu_tanh(acc[r] + bb)));
     }
     __syncthreads();
 
-    // (3) c_proj slice: thread t owns output columns (t + 256 i + rot) mod K; fixed-order 16-deep dot
-    //     per row.  rot staggers the workgroups' column order so their atomics to one address do not
-    //     arrive together (same-address atomics serialise at the memory side)
+    // (3) c_proj slice: thread t owns output columns (t + 256 i + rot) mod K; fixed-order dot over
+    //     the workgroup's 16 CG intermediate columns per row.  rot staggers the workgroups' column
+    //     order so their atomics to one address do not arrive together
     unsigned long long* rc = r_out + (size_t)(blockIdx.x % DLMS_FIX_COPIES) * rcs;
     const int rot = (int)((blockIdx.x / DLMS_FIX_COPIES) * 64 % K);
 #pragma unroll
-    for (int i = 0; i < NC; ++i) {
+    for (int i = 0; i < NCP; ++i) {
         int n = tid + 256 * i;
         if (n >= K) continue;
         n = n + rot < K ? n + rot : n + rot - K;
-        float w[16];
-        unpack8(*reinterpret_cast<const uint4*>(wp_lds + n * 32), w);
-        unpack8(*reinterpret_cast<const uint4*>(wp_lds + n * 32 + 16), w + 8);
-        for (int m = 0; m < M; ++m) {
-            float o = 0.f;
+        float o[ROWS];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) o = fmaf(hs[m][k], w[k], o);
-            if (blockIdx.x == 0) o += v_lds[m * K + n] + bp[i];  // the residual and the c_proj bias, once
-            atomicAdd(rc + (size_t)m * ldr + n, f32_to_fix(o));
+        for (int m = 0; m < ROWS; ++m) o[m] = 0.f;
+#pragma unroll
+        for (int c = 0; c < CG; ++c) {
+            float w[16];
+            const char* wr = wp_lds + ((size_t)c * K + n) * 32;
+            unpack8(*reinterpret_cast<const uint4*>(wr), w);
+            unpack8(*reinterpret_cast<const uint4*>(wr + 16), w + 8);
+#pragma unroll
+            for (int m = 0; m < ROWS; ++m) {
+                if (m >= M) break;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) o[m] = fmaf(hs[m][16 * c + k], w[k], o[m]);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < ROWS; ++m) {
+            if (m >= M) break;
+            float v = o[m];
+            if (blockIdx.x == 0) v += v_lds[m * K + n] + bp[i];  // the residual and the c_proj bias, once
+            atomicAdd(rc + (size_t)m * ldr + n, f32_to_fix(v));
         }
     }
 }
 
-template <int NSPLIT, int NV4, int RPW, int NC, bool XFIX>
+template <int NSPLIT, int NV4, int RPW, int NKB, int CG, bool XFIX>
 static hipError_t launch_mlp(const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
                              const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
                              const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* r_out, int ldr,
-                             long long rcs, long long xcs, int M, int K, int F, hipStream_t stream) {
-    constexpr int KBW = NV4 <= 2 ? 4 : 8;  // >= K/32/4 for K <= 256 * NV4 (NV4 <= 4)
-    // LN image (1-KiB aligned) + W_p slice + block 0's residual rows
-    const size_t lds = (((size_t)16 * (K * 2 + 16) + 1023) & ~(size_t)1023) + (size_t)K * 32 + (size_t)4 * RPW * K * 4;
-    static bool attr_set = false;
-    if (!attr_set && lds > 65536) {
-        // (the kernel's static LDS comes on top: ask for what the largest K of this instantiation needs)
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_mlp_kernel<NSPLIT, NV4, RPW, KBW, NC, XFIX>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
+                             long long rcs, long long xcs, int M, int F, hipStream_t stream) {
+    if constexpr (!mlp_fits(RPW, NKB, CG)) {
+        return hipErrorInvalidValue;
+    } else {
+        if (F % (16 * CG)) return hipErrorInvalidValue;
+        constexpr int lds = mlp_dyn_lds(RPW, NKB, CG);
+        static bool attr_set = false;
+        if (!attr_set && lds > 65536) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_mlp_kernel<NSPLIT, NV4, RPW, NKB, CG, XFIX>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e != hipSuccess) return e;
+            attr_set = true;
+        }
+        hipLaunchKernelGGL((skinny_mlp_kernel<NSPLIT, NV4, RPW, NKB, CG, XFIX>), dim3(F / (16 * CG)), dim3(256), lds, stream,
+                           x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, r_out, ldr, rcs, xcs, M);
+        return hipGetLastError();
     }
-    hipLaunchKernelGGL((skinny_mlp_kernel<NSPLIT, NV4, RPW, KBW, NC, XFIX>), dim3(F / 16), dim3(256), lds, stream, x_in,
-                       ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, r_out, ldr, rcs, xcs, M, K);
-    return hipGetLastError();
 }
 
 // x_in: f32 (xfix = 0) or int64 fixed point [M][ldx]; parts: nsplit (0 or 4) f32 slabs; Wfc_sh:
 // shuffle_weight(W_fc) [F/16][K/32][64][8]; Wp_sl [F/16][K][16]; r_out int64 [M][ldr], zeroed.
 extern "C" int dlms_fix_copies() { return DLMS_FIX_COPIES; }
 
+// column groups per workgroup: DLMS_MLP_CG (1, 2 or 4; 0 = per width default)
+static int mlp_cg_env() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DLMS_MLP_CG");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
+// the CG a launch uses: the requested one when it fits the LDS at this row count, else the widest
+// that does (the kernel's CG * K * 32 B W_p slices + LN image + block 0's residual rows)
+extern "C" int dlms_skinny_mlp_cg(int K, int M, int want) {
+    const int nkb = K / 32;
+    const int rpw = M <= 4 ? 1 : 2;
+    if (want <= 0) want = mlp_cg_env();
+    if (want <= 0) want = K <= 1024 ? 4 : 2;
+    for (int cg = want; cg >= 1; cg /= 2)
+        if (mlp_fits(rpw, nkb, cg)) return cg;
+    return 0;
+}
+
+template <int NSPLIT, int NV4, int NKB, bool XFIX, int RPW>
+static hipError_t mlp_cg(int cg, const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
+                         const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
+                         const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* R, int ldr,
+                         long long rcs, long long xcs, int M, int F, hipStream_t stream) {
+#define MLP_GO(CG_) \
+    return launch_mlp<NSPLIT, NV4, RPW, NKB, CG_, XFIX>(x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, \
+                                                       b_p, R, ldr, rcs, xcs, M, F, stream)
+    switch (cg) {
+        case 1: MLP_GO(1);
+        case 2: MLP_GO(2);
+        case 4: MLP_GO(4);
+        default: return hipErrorInvalidValue;
+    }
+#undef MLP_GO
+}
+
+template <int NSPLIT, int NV4, int NKB>
+static hipError_t mlp_rows(int cg, int xfix, const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
+                           const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
+                           const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* R, int ldr,
+                           long long rcs, long long xcs, int M, int F, hipStream_t stream) {
+#define MLP_ARGS cg, x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, R, ldr, rcs, xcs, M, F, stream
+    if (M <= 4) {
+        if (xfix) return mlp_cg<NSPLIT, NV4, NKB, true, 1>(MLP_ARGS);
+        return mlp_cg<NSPLIT, NV4, NKB, false, 1>(MLP_ARGS);
+    }
+    if constexpr (NV4 <= 4 && NSPLIT <= 4) {
+        if (xfix) return mlp_cg<NSPLIT, NV4, NKB, true, 2>(MLP_ARGS);
+        return mlp_cg<NSPLIT, NV4, NKB, false, 2>(MLP_ARGS);
+    }
+    return hipErrorInvalidValue;
+#undef MLP_ARGS
+}
+
 // r_out / a fixed-point x_in: DLMS_FIX_COPIES copies [copy][M][ld], copy strides rcs / xcs (elements)
 extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long long xcs, const float* parts, int ldp,
                                       long long split_stride, int nsplit, const float* res_bias, const float* gamma,
                                       const float* beta, float eps, const void* Wfc_sh, const float* b_fc,
                                       const void* Wp_sl, const float* b_p, void* r_out, int ldr, long long rcs, int M,
-                                      int K, int F, hipStream_t stream) {
-    if (M <= 0 || M > 8 || K % 256 || K > 1024 || F % 16 || F <= 0) return hipErrorInvalidValue;
-    if (nsplit != 0 && nsplit != 4) return hipErrorInvalidValue;
+                                      int K, int F, int want_cg, hipStream_t stream) {
+    if (M <= 0 || M > 8 || F % 16 || F <= 0) return hipErrorInvalidValue;
+    if (nsplit != 0 && (nsplit != 4 || K > 1024)) return hipErrorInvalidValue;
+    const int cg = dlms_skinny_mlp_cg(K, M, want_cg);
+    if (cg == 0) return hipErrorInvalidValue;
     const bf16_t* Wf = reinterpret_cast<const bf16_t*>(Wfc_sh);
     const bf16_t* Wp = reinterpret_cast<const bf16_t*>(Wp_sl);
     unsigned long long* R = reinterpret_cast<unsigned long long*>(r_out);
-#define MLP_GO(NS, NV, RPW_, NC_, XF) \
-    return launch_mlp<NS, NV, RPW_, NC_, XF>(x_in, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, Wf, b_fc, \
-                                            Wp, b_p, R, ldr, rcs, xcs, M, K, F, stream)
-#define MLP_RPW(NS, NV, NC_, XF) \
-    if (M <= 4) MLP_GO(NS, NV, 1, NC_, XF); else MLP_GO(NS, NV, 2, NC_, XF);
-#define MLP_X(NS, NV, NC_) \
-    if (xfix) { MLP_RPW(NS, NV, NC_, true) } else { MLP_RPW(NS, NV, NC_, false) }
+#define MLP_K(NS, NV, NKB_) \
+    return mlp_rows<NS, NV, NKB_>(cg, xfix, x_in, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, Wf, b_fc, Wp, \
+                                  b_p, R, ldr, rcs, xcs, M, F, stream)
     switch (K) {
         case 768:
-            if (nsplit == 4) { MLP_X(4, 3, 3) } else { MLP_X(0, 3, 3) }
+            if (nsplit == 4) MLP_K(4, 3, 24);
+            MLP_K(0, 3, 24);
         case 1024:
-            if (nsplit == 4) { MLP_X(4, 4, 4) } else { MLP_X(0, 4, 4) }
+            if (nsplit == 4) MLP_K(4, 4, 32);
+            MLP_K(0, 4, 32);
+        case 1280: MLP_K(0, 5, 40);
+        case 1600: MLP_K(0, 7, 50);
         default: return hipErrorInvalidValue;
     }
-#undef MLP_X
-#undef MLP_RPW
-#undef MLP_GO
+#undef MLP_K
 }
 
 // Final LayerNorm of the fixed-point residual (ln_f after a fused MLP): one wave per row -> bf16.

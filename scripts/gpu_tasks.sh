@@ -10,6 +10,7 @@
 #   bench            default bench.py (headline + b1/b32 keys)    -> gpurun_out/bench.log
 #   prof:<tag>       rocprofv3 kernel stats of a short bench.py run (B=1024)   -> gpurun_out/prof_<tag>/
 #   prof1:<tag>      the same at batch 1
+#   profm:<tag>:<model>:<batch>  the same for another model / batch
 #   pmc:<tag>:<batch>  three rocprofv3 --pmc passes (SQ / TCC fetch / TCC write) of an eager bench.py run
 #                    -> gpurun_out/pmc_<tag>/summary.json
 #   trace:<tag>      per-dispatch kernel trace of one B=1024 generation (timeline analysis) -> gpurun_out/trace_<tag>/
@@ -67,6 +68,9 @@ for task in "$@"; do
         prof:*) prof "${task#prof:}" --steps 5 --warmup 2 --latency-batches "" ;;
         prof1:*) prof "${task#prof1:}" --batch 1 --steps 3 --warmup 1 --latency-batches "" ;;
         prof32:*) prof "${task#prof32:}" --batch 32 --steps 3 --warmup 1 --latency-batches "" ;;
+        profm:*)  # profm:<tag>:<model>:<batch>
+            spec=${task#profm:}; tag=${spec%%:*}; rest=${spec#*:}; model=${rest%%:*}; batch=${rest#*:}
+            prof "$tag" --model "$model" --batch "$batch" --steps 3 --warmup 1 --latency-batches "" ;;
         pmc:*)
             spec=${task#pmc:}; tag=${spec%%:*}; batch=${spec#*:}; export TMPDIR=/tmp; D=gpurun_out/pmc_$tag; mkdir -p $D
             passes=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"

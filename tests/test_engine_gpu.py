@@ -95,7 +95,7 @@ def test_latency_path_matches_tiled_path():
     _assert_teacher_forced(ref, slow.generate(prompts), prompts)
 
 
-@pytest.mark.parametrize("name", ["gpt2", "gpt2-medium"])
+@pytest.mark.parametrize("name", ["gpt2", "gpt2-medium", "gpt2-large", "gpt2-xl"])
 def test_fused_mlp_batch1(name, monkeypatch):
     """Batch 1 runs LN2 -> c_fc -> GELU -> c_proj as one kernel into the int64 fixed-point residual:
     exact under the margin rule against the fp32 oracle, identical across graph replay / eager and

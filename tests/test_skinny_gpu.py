@@ -364,13 +364,17 @@ def _to_fix(x):
 
 
 @pytest.mark.parametrize("M", [1, 2, 5, 8])
-@pytest.mark.parametrize("K", [768, 1024])
-@pytest.mark.parametrize("nsplit,xfix", [(4, False), (4, True), (0, True)])
-def test_skinny_mlp(M, K, nsplit, xfix):
+@pytest.mark.parametrize("K", [768, 1024, 1280, 1600])
+@pytest.mark.parametrize("nsplit,xfix", [(4, False), (4, True), (0, True), (0, False)])
+def test_skinny_mlp(M, K, nsplit, xfix, cg=0):
     """Fused MLP: r_out += fix(v + gelu(LN(v) W_fc^T + b_fc) W_p^T + b_p), v = x + res_bias + sum(parts),
     against fp32 (with the same bf16 roundings of LN(v) and h), and bit-identical over repeated launches
-    (the workgroups' 64-bit integer atomics commute)."""
+    (the workgroups' 64-bit integer atomics commute).  GPT-2 small .. XL widths (r3)."""
     ops = _ops()
+    if nsplit and K > 1024:
+        pytest.skip("head-group slabs: d <= 1024 only")
+    if ops.skinny_mlp_cg(K, M, cg) == 0:
+        pytest.skip(f"{M} rows of width {K} do not fit the fused MLP")
     F = 4 * K
     x = _rand(M, K, seed=201, dtype=torch.float32) * 2
     parts = _rand(4, M, K, seed=202, dtype=torch.float32) * 0.5
@@ -387,7 +391,7 @@ def test_skinny_mlp(M, K, nsplit, xfix):
     for _ in range(3):
         r = torch.zeros(ops.fix_copies(), M, K, dtype=torch.int64, device=DEV)
         ops.skinny_mlp(x_in, g, b, 1e-5, w_fc_sh, b_fc, w_p_sl, b_p, r, parts=parts if nsplit else None,
-                       nsplit=nsplit, res_bias=rb)
+                       nsplit=nsplit, res_bias=rb, cg=cg)
         outs.append(r)
     assert all(torch.equal(outs[0], o) for o in outs[1:]), "fixed-point accumulation must be order-independent"
     v = x_used + rb + parts[:nsplit].sum(0)
@@ -395,6 +399,15 @@ def test_skinny_mlp(M, K, nsplit, xfix):
     ff = torch.nn.functional.gelu(h @ w_fc.float().t() + b_fc, approximate="tanh").to(torch.bfloat16).float()
     ref = v + ff @ w_p.float().t() + b_p
     torch.testing.assert_close(ops.fix_to_float(outs[0]), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("K", [768, 1024, 1280, 1600])
+@pytest.mark.parametrize("cg", [1, 2, 4])
+@pytest.mark.parametrize("M", [1, 6])
+def test_skinny_mlp_column_groups(M, K, cg):
+    """Every column-group width of the fused MLP (workgroups owning 16, 32 or 64 intermediate
+    columns) against the fp32 reference (narrowed to what fits the LDS at this width)."""
+    test_skinny_mlp(M, K, 0, False, cg=cg)
 
 
 def test_skinny_mlp_adds_into_accumulator():
