@@ -168,7 +168,12 @@ __device__ __forceinline__ float gelu_tanh(float x) {
     const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
     const float k1 = 0.044715f;
     float u = k0 * (x + k1 * x * x * x);
-    return 0.5f * x * (1.0f + tanhf(u));
+    // 0.5 x (1 + tanh(u)) == x * sigmoid(2u) == x / (1 + e^(-2u)): one v_exp_f32 + one v_rcp_f32
+    // instead of libm tanhf (~40 VALU ops: the GELU epilogue of the 32768-row prefill c_fc was
+    // VALU-bound).  |rel err| ~1e-6 before the bf16 rounding of every consumer; e^(-2u) = inf for
+    // very negative u gives x * 0 = -0, the limit.
+    const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * u);  // e^(-2u) = 2^(-2u log2 e)
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
 __device__ __forceinline__ float gelu_erf(float x) {

@@ -436,6 +436,16 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
             default: break;
         }
     }
+    // 64x96 tiles (waves 32x48): decode row halves (M 512) get one round of <= 256 workgroups on the
+    // GPT-2 widths (N 2304 -> 192 tiles, N 3072 -> 256), so no CU streams two tiles' operands
+    if (N % 96 == 0) {
+        switch (id) {
+            case 17: return launch_gemm_cfg<64, 96, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 18: return launch_gemm_cfg<64, 96, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 19: return launch_gemm_cfg<64, 96, 2, 2, 6, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+            default: break;
+        }
+    }
     if (N % 256 == 0 && id == 9) return launch_gemm_cfg<128, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     // 256x256, 8 waves of 128x64 (the cdna guide's big-tile geometry, on this kernel's 1-barrier loop)
     // (not for the fp32 split-K epilogue: its 256 x 1 KiB staged rows exceed the LDS)

@@ -883,6 +883,7 @@ static int mlp_cg_env() {
 extern "C" int dlms_skinny_mlp_cg(int K, int M, int want) {
     const int nkb = K / 32;
     const int rpw = M <= 4 ? 1 : 2;
+    if (rpw == 2 && K > 1024) return 0;  // mlp_rows: 8-row images only up to d 1024 (VGPR budget)
     if (want <= 0) want = mlp_cg_env();
     if (want <= 0) want = K <= 1024 ? 4 : 2;
     for (int cg = want; cg >= 1; cg /= 2)

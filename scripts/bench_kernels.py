@@ -21,7 +21,7 @@ from distributed_lms_raft_llm_amd import ops  # noqa: E402
 TILES = {-1: "auto", 0: "32x64s6", 1: "64x64s4", 2: "128x64s3", 3: "128x128s3", 4: "64x64s2", 5: "64x128s3",
          6: "128x128s2", 7: "64x64s6", 8: "256x128w8s2", 9: "128x256w8s2", 10: "128x128w8s3(4x2)",
          11: "128x128w8s3(2x4)", 12: "256x128s2(wave128x64)", 13: "256x128s3(wave128x64)",
-         14: "256x256w8s2(wave128x64)"}
+         14: "256x256w8s2(wave128x64)", 17: "64x96s4", 18: "64x96s3", 19: "64x96s6"}
 
 
 def graph_time(fn, inner=20, reps=15):
