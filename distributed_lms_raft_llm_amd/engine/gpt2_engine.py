@@ -211,6 +211,11 @@ class HipGPT2Engine:
         # stream batches keep the heuristic (cap 2 costs 3 % at 256, 8 % at 64).
         # profiles/r1_split_cap_insitu.log; DLMS_OVERLAP_SPLIT_CAP overrides.
         self.overlap_split_cap = int(os.environ.get("DLMS_OVERLAP_SPLIT_CAP", "2"))
+        self.gemm96 = os.environ.get("DLMS_GEMM96", "1") != "0"  # gemm.hip gemm96_on(): same switch
+        # DLMS_TIMING_SKIP=attn|gemm|ln: TIMING-ONLY differential experiment (tokens are garbage): drop
+        # the decode attention, the GEMM-side kernels (LN + GEMMs) or only the LayerNorms from every
+        # decode step to see which side bounds it
+        self._timing_skip = os.environ.get("DLMS_TIMING_SKIP", "")
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
         # decode steps per graph replay in the overlapped step: the row parts run that many steps each
         # on their own stream before joining (rows are independent sequences), so a part that gets
@@ -444,6 +449,11 @@ class HipGPT2Engine:
             return parts, 1, bias
         if fixed:
             s = max(d for d in range(1, fixed + 1) if (w.shape[1] // 64) % d == 0)
+        elif self.gemm96 and 256 < M <= 512 and w.shape[1] >= 2048 and w.shape[0] % 96 == 0 and \
+                (w.shape[1] // 64) % 4 == 0:
+            # c_proj on a 512-row decode half: split 4 -> 64x96 tiles in one round of 256 workgroups
+            # (the launcher's DLMS_GEMM96 rule): 10.5 -> 8.5 us alone, profiles/r3_kern_sweep_m512.jsonl
+            s = 4
         else:
             s = self._split(M, w.shape[0], w.shape[1], cap)
         ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=s)
@@ -463,6 +473,10 @@ class HipGPT2Engine:
 
     def _attn_in(self, r: "_Rows", li: int):
         """LN1 (folding the pending residual update) -> QKV GEMM (+ K/V scattered into the cache)."""
+        if self._timing_skip in ("gemm", "ln") and r.tiles is None:  # timing-only experiment: see __init__
+            if self._timing_skip == "ln":
+                self._attn_in_gemm_only(r, li)
+            return
         lw, eps, pend = self.w.layers[li], self.cfg.layer_norm_epsilon, r.pend
         kc, vc = self.kv[li, 0], self.kv[li, 1]
         ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
@@ -473,7 +487,14 @@ class HipGPT2Engine:
             ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
                      row_slot=r.row_slot, row_pos=r.row_pos)
 
+    def _attn_in_gemm_only(self, r: "_Rows", li: int):
+        lw = self.w.layers[li]
+        ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=self.kv[li, 0], v_cache=self.kv[li, 1],
+                 row_slot=r.row_slot, row_pos=r.row_pos)
+
     def _attn(self, r: "_Rows", li: int):
+        if self._timing_skip == "attn" and r.tiles is None:  # timing-only experiment: see __init__
+            return
         if r.tiles is not None:  # packed prompts (K6): 16-query MFMA tiles
             ops.tile_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, r.tiles, out=r.att)
         elif r.M * self.w.n_heads_local <= self.SPLIT_ATTN_MAX_PAIRS:
@@ -494,6 +515,13 @@ class HipGPT2Engine:
 
     def _attn_out_mlp(self, r: "_Rows", li: int):
         """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
+        if self._timing_skip in ("gemm", "ln") and r.tiles is None:  # timing-only experiment: see __init__
+            if self._timing_skip == "ln":
+                lw = self.w.layers[li]
+                r.pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M, r.split_cap, r.split_fixed)
+                ops.gemm(r.h, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff)
+                r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap, r.split_fixed)
+            return
         lw, eps = self.w.layers[li], self.cfg.layer_norm_epsilon
         pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M, r.split_cap, r.split_fixed)
         ops.add_layernorm(r.x, lw.ln2_g, lw.ln2_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)

@@ -25,6 +25,7 @@
 //                   no atomics) -- the decode projections with N = d are split 2-4 ways so the
 //                   latency-bound skinny GEMMs put enough workgroups on the 256 CUs.
 #include "common.h"
+#include <stdlib.h>
 
 enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6 };
 
@@ -402,7 +403,15 @@ static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw
 // 64x64 workgroups are latency-bound on the K loop: keep 4-6 stages of LDS-DMA in flight; above
 // that, occupancy hides latency better than ring depth (2 stages, two workgroups per CU).  The LM
 // head (N = vocab) and prefill grids amortise 128x128 tiles.  8-wave variants stay tuning-only.
-static int g_force_tile = -1;  // tuning override (dlms_gemm_force_tile), -1 = heuristic
+static int g_force_tile = -1;
+static bool gemm96_on() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DLMS_GEMM96");
+        v = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}  // tuning override (dlms_gemm_force_tile), -1 = heuristic
 
 template <int EPI, int IN>
 static hipError_t launch_forced(int id, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
@@ -487,6 +496,16 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
         if (K >= 1024 && M >= 256 && t128x64 <= 256)
             return launch_gemm_cfg<128, 64, 2, 2, 3, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     }
+    // decode row halves of the overlapped step (256 < M <= 512, K = 768 / 3072): 64x96 tiles in ONE
+    // round of <= 256 workgroups -- QKV 192, c_fc 256, c_proj split 4 -> 256 -- so no CU streams two
+    // tiles' operands (profiles/r3_kern_sweep_m512.jsonl: QKV 9.7 -> 8.5 us, c_fc 10.2 -> 8.7 us,
+    // c_proj split-2 10.5 -> split-4 8.5 us); DLMS_GEMM96=0 turns it off (A/B)
+    if (gemm96_on() && N % 96 == 0 && M > 256 && M <= 512 && N != 768 &&
+        (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_QKV || (EPI == EPI_PARTIAL && split == 4)) &&
+        (long)((M + 63) / 64) * (N / 96) * split <= 256)
+        return launch_gemm_cfg<64, 96, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    if (EPI == EPI_PARTIAL && gemm96_on() && N == 768 && split == 4 && M > 256 && M <= 512 && K >= 2048)
+        return launch_gemm_cfg<64, 96, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
         return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     // few-row LM head (latency path, B <= 32): 32-row A tiles, so clamped copies of the few real rows

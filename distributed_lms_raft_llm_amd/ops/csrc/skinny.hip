@@ -885,7 +885,9 @@ extern "C" int dlms_skinny_mlp_cg(int K, int M, int want) {
     const int rpw = M <= 4 ? 1 : 2;
     if (rpw == 2 && K > 1024) return 0;  // mlp_rows: 8-row images only up to d 1024 (VGPR budget)
     if (want <= 0) want = mlp_cg_env();
-    if (want <= 0) want = K <= 1024 ? 4 : 2;
+    // per-width/rows default (in situ, bench.py --batch 1/2 on one box, profiles/r3_sweep_gemm96_mlp_cg.txt):
+    // d <= 1024, 1 row: CG 2 30.9 ms vs CG 4 34.5 / CG 1 31.8; 2 rows: CG 1 33.5 vs 34.7 / 38.0
+    if (want <= 0) want = K <= 1024 ? (M <= 1 ? 2 : 1) : 2;
     for (int cg = want; cg >= 1; cg /= 2)
         if (mlp_fits(rpw, nkb, cg)) return cg;
     return 0;
