@@ -99,6 +99,7 @@ class _Rows:
     split_fixed: int | None = None  # pinned split-K (M-independent arithmetic: prefill_split)
     persist_attn: bool = False  # decode attention as the low-occupancy persistent kernel
     part: bool = False  # one of several concurrent row parts (no shared-workspace kernels)
+    pidx: int = 0  # index of the row part (timing-only experiments address parts by it)
 
 
 class HostResult:
@@ -215,7 +216,13 @@ class HipGPT2Engine:
         # DLMS_TIMING_SKIP=attn|gemm|ln: TIMING-ONLY differential experiment (tokens are garbage): drop
         # the decode attention, the GEMM-side kernels (LN + GEMMs) or only the LayerNorms from every
         # decode step to see which side bounds it
+        # per-part form "p0:attn+p1:gemm" (mode all = attention + GEMM side)
         self._timing_skip = os.environ.get("DLMS_TIMING_SKIP", "")
+        self._timing_skip_part = {}
+        for item in self._timing_skip.replace("+", ",").split(","):
+            if item.startswith("p") and ":" in item:
+                i, m = item[1:].split(":", 1)
+                self._timing_skip_part[int(i)] = m
         self.overlap_parts = int(os.environ.get("DLMS_OVERLAP_PARTS", "2")) if overlap_parts is None else overlap_parts
         # decode steps per graph replay in the overlapped step: the row parts run that many steps each
         # on their own stream before joining (rows are independent sequences), so a part that gets
@@ -239,6 +246,17 @@ class HipGPT2Engine:
         # (batch 1: 37.3 vs 35.9 ms per query, profiles/r2_lm_head_b1.txt)
         self.lm_ln_fused = os.environ.get("DLMS_LM_LN_FUSED", "0") == "1"
         self.alt_attn = os.environ.get("DLMS_OVERLAP_ALT_ATTN", "0") == "1"
+        # overlapped step, TP=1 bf16: LN2 folded into c_fc (ops.fold_ln_weights / EPI_GELU_LN) -- the
+        # out-projection updates the residual in place and leaves a bf16 copy, c_fc normalises
+        # algebraically from its own A fragments: one launch fewer per layer and row part.  OPT-IN:
+        # measured 5 % slower at 1024 queries (688-690 vs 724 k tok/s, profiles/r3_fold_ln2_and_interference.jsonl):
+        # the out-projection loses its split-K (32x64 full-K tiles, 147 KB per workgroup) and c_fc's
+        # K loop carries the statistics, which together cost more than the LayerNorm launch saved
+        self.fold_ln2 = (os.environ.get("DLMS_FOLD_LN2", "0") == "1" and self.tp_size == 1 and not self.w.fp8
+                         and self.overlap)
+        self._ln2_fold = None
+        if self.fold_ln2:
+            self._ln2_fold = [ops.fold_ln_weights(lw.ln2_g, lw.ln2_b, lw.w_fc, lw.b_fc) for lw in self.w.layers]
         # 16-32 rows: this many latency-path parts on as many HIP streams (0/1 = off)
         self.small_overlap_parts = int(os.environ.get("DLMS_SMALL_OVERLAP_PARTS", "0"))  # measured slower (docs/PERFORMANCE.md)
         self._in_small_overlap = False
@@ -473,8 +491,8 @@ class HipGPT2Engine:
 
     def _attn_in(self, r: "_Rows", li: int):
         """LN1 (folding the pending residual update) -> QKV GEMM (+ K/V scattered into the cache)."""
-        if self._timing_skip in ("gemm", "ln") and r.tiles is None:  # timing-only experiment: see __init__
-            if self._timing_skip == "ln":
+        if self._skip(r) in ("gemm", "ln", "all"):  # timing-only experiment: see __init__
+            if self._skip(r) == "ln":
                 self._attn_in_gemm_only(r, li)
             return
         lw, eps, pend = self.w.layers[li], self.cfg.layer_norm_epsilon, r.pend
@@ -487,13 +505,19 @@ class HipGPT2Engine:
             ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
                      row_slot=r.row_slot, row_pos=r.row_pos)
 
+    def _skip(self, r: "_Rows") -> str:
+        """Timing-only skip mode for this row range (DLMS_TIMING_SKIP; never set in production)."""
+        if not self._timing_skip or r.tiles is not None:
+            return ""
+        return self._timing_skip_part.get(r.pidx, "") if self._timing_skip_part else self._timing_skip
+
     def _attn_in_gemm_only(self, r: "_Rows", li: int):
         lw = self.w.layers[li]
         ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=self.kv[li, 0], v_cache=self.kv[li, 1],
                  row_slot=r.row_slot, row_pos=r.row_pos)
 
     def _attn(self, r: "_Rows", li: int):
-        if self._timing_skip == "attn" and r.tiles is None:  # timing-only experiment: see __init__
+        if self._skip(r) in ("attn", "all"):  # timing-only experiment: see __init__
             return
         if r.tiles is not None:  # packed prompts (K6): 16-query MFMA tiles
             ops.tile_attention(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, r.tiles, out=r.att)
@@ -515,8 +539,17 @@ class HipGPT2Engine:
 
     def _attn_out_mlp(self, r: "_Rows", li: int):
         """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
-        if self._timing_skip in ("gemm", "ln") and r.tiles is None:  # timing-only experiment: see __init__
-            if self._timing_skip == "ln":
+        if r.persist_attn and self._ln2_fold is not None and not self._skip(r):
+            # LN2 folded into c_fc: x += att W_o^T + b_o in place (+ bf16 copy into h, which the QKV
+            # GEMM has consumed), then c_fc normalises its raw A rows algebraically
+            lw = self.w.layers[li]
+            wp, c1, c2 = self._ln2_fold[li]
+            ops.gemm(r.att, lw.w_o, ops.EPI_F32X2, bias=lw.b_o, resid=r.x, out=r.x, out2=r.h)
+            ops.gemm(r.h, wp, ops.EPI_GELU_LN, bias=c2, ln_c1=c1, ln_eps=self.cfg.layer_norm_epsilon, out=r.ff)
+            r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap, r.split_fixed)
+            return
+        if self._skip(r) in ("gemm", "ln", "all"):  # timing-only experiment: see __init__
+            if self._skip(r) == "ln":
                 lw = self.w.layers[li]
                 r.pend = self._row_parallel(r.att, lw.w_o, lw.b_o, r.parts, r.M, r.split_cap, r.split_fixed)
                 ops.gemm(r.h, lw.w_fc, ops.EPI_GELU_TANH, bias=lw.b_fc, out=r.ff)
@@ -608,6 +641,7 @@ class HipGPT2Engine:
                           self.h8[lo:hi] if fp8 else None, self.hsc[lo:hi] if fp8 else None)
         r.split_cap = self.overlap_split_cap
         r.persist_attn = self.persist_attn_blocks > 0
+        r.pidx = lo // max(1, hi - lo)
         return r
 
     def _part_step(self, r: "_Rows", lo: int, penalty: float):

@@ -35,7 +35,7 @@ SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "en
            "dataflow.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
-EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
+EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL, EPI_F32X2, EPI_GELU_LN = range(9)
 
 _lock = threading.Lock()
 _lib = None
@@ -118,6 +118,7 @@ class GemmEpi(ctypes.Structure):
         ("split_k", ctypes.c_int), ("split_stride", ctypes.c_longlong),
         ("a_scale", ctypes.c_void_p), ("w_scale", ctypes.c_void_p),
         ("n_slots", ctypes.c_int),
+        ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int), ("ln_c1", ctypes.c_void_p), ("ln_eps", ctypes.c_float),
     ]
 
 
@@ -284,7 +285,7 @@ def _req(t: torch.Tensor, dtype, name: str, dim: int | None = None):
 def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, out=None, resid=None,
          q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
          argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0,
-         split_k: int = 1, a_scale=None, w_scale=None):
+         split_k: int = 1, a_scale=None, w_scale=None, out2=None, ln_c1=None, ln_eps: float = 1e-5):
     """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0).
     fp8 (W8A8): a and w ``torch.float8_e4m3fn`` with f32 ``a_scale`` [M] and ``w_scale`` [N]
     (C = diag(a_scale) (a @ w.T) diag(w_scale)); K % 128 == 0."""
@@ -308,8 +309,20 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         if bias.numel() < N:
             raise ValueError("bias too short")
         ep.bias = bias.data_ptr()
-    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32):
-        want = torch.float32 if epi == EPI_F32 else torch.bfloat16
+    if epi in (EPI_F32X2, EPI_GELU_LN) and fp8:
+        raise ValueError("EPI_F32X2 / EPI_GELU_LN: bf16 inputs only")
+    if epi == EPI_F32X2:
+        _req(out2, torch.bfloat16, "out2", 2)
+        if out2.shape[0] < M or out2.shape[1] < N or out2.stride(1) != 1:
+            raise ValueError("out2 too small")
+        ep.out2, ep.ldo2 = out2.data_ptr(), out2.stride(0)
+    if epi == EPI_GELU_LN:
+        _req(ln_c1, torch.float32, "ln_c1", 1)
+        if ln_c1.numel() < N:
+            raise ValueError("ln_c1 too short")
+        ep.ln_c1, ep.ln_eps = ln_c1.data_ptr(), float(ln_eps)
+    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_F32X2, EPI_GELU_LN):
+        want = torch.float32 if epi in (EPI_F32, EPI_F32X2) else torch.bfloat16
         if out is None:
             out = torch.empty(M, N, dtype=want, device=a.device)
         _req(out, want, "out", 2)
@@ -699,6 +712,19 @@ def cosine(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-8, out=None):
 # Skinny (M <= 32) decode GEMMs on pre-shuffled weights + split-K flash-decode (skinny.hip)
 # ---------------------------------------------------------------------------------------------
 SKINNY_MAX_M = 32
+
+
+def fold_ln_weights(gamma: torch.Tensor, beta: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None):
+    """LayerNorm folded into the following GEMM (``EPI_GELU_LN``): LN(x) W^T + b = rstd (x W'^T - mu c1)
+    + c2 with W' = bf16(gamma (.) W) (the operand the MFMAs see), c1 = row sums of that bf16 W' in
+    fp32, c2 = beta W^T + b.  w: bf16 [N, K]; gamma, beta: f32 [K].  Returns (W', c1, c2)."""
+    wf = w.float()
+    wp = (wf * gamma.float()[None, :]).to(torch.bfloat16)
+    c1 = wp.float().sum(dim=1).contiguous()
+    c2 = wf @ beta.float()
+    if b is not None:
+        c2 = c2 + b.float()
+    return wp.contiguous(), c1, c2.contiguous()
 
 
 def shuffle_weight(w: torch.Tensor) -> torch.Tensor:

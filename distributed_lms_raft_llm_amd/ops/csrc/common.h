@@ -299,4 +299,9 @@ struct GemmEpi {
     const float* a_scale;
     const float* w_scale;
     int n_slots;  // EPI_QKV: KV-cache slots (the checked build range-checks row_slot against it)
+    // EPI_F32X2: bf16 copy of the f32 output; EPI_GELU_LN: c1 = row sums of gamma (.) W, LN epsilon
+    bf16_t* out2;
+    int ldo2;
+    const float* ln_c1;
+    float ln_eps;
 };

@@ -20,6 +20,14 @@
 //   128-B LDS rows then hold 128 k-elements, each 16-B fragment feeds two
 //   v_mfma_f32_16x16x32_fp8_fp8, and acc is rescaled by a_scale[row] * w_scale[col] before the
 //   epilogue.  W8A8 halves the weight bytes the latency-bound decode GEMMs stream.)
+//   EPI_F32X2       out = f32(acc + bias + resid) AND out2 = bf16(out)   out-projection whose result
+//                                                                feeds a LayerNorm-folded GEMM (below)
+//   EPI_GELU_LN     out = bf16(gelu(rstd_m (acc - mu_m c1_n) + bias_n)): c_fc with LN2 FOLDED IN.  A is
+//                   the raw residual row (bf16), W = gamma (.) W_fc; the K loop covers the whole row,
+//                   so each workgroup accumulates its rows' sum / sum of squares from the very A
+//                   fragments it feeds the MFMAs (mu, rstd), and LN(x) W^T = rstd (x W'^T - mu c1) +
+//                   beta W^T with c1 = row sums of W' and bias = beta W_fc^T + b_fc: no LayerNorm
+//                   launch between the out-projection and c_fc (ops.fold_ln_weights)
 //   EPI_PARTIAL     split-K: slice s stores its raw fp32 partial tile; the following fused
 //                   residual-add + LayerNorm kernel sums the slices in a fixed order (deterministic,
 //                   no atomics) -- the decode projections with N = d are split 2-4 ways so the
@@ -27,7 +35,8 @@
 #include "common.h"
 #include <stdlib.h>
 
-enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6 };
+enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6,
+       EPI_F32X2 = 7, EPI_GELU_LN = 8 };
 
 // struct GemmEpi lives in common.h (shared with the ABI probe in api.hip)
 
@@ -122,6 +131,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+    float ln_s1[TM], ln_s2[TM];  // EPI_GELU_LN: this lane's k-share of its A rows' sum / sum of squares
+#pragma unroll
+    for (int i = 0; i < TM; ++i) ln_s1[i] = ln_s2[i] = 0.f;
+    __shared__ float2 ln_stat[EPI == EPI_GELU_LN ? BM : 1];  // (mean, rstd) per tile row
+
     const int nk = k_len / BKE;
     // prologue: up to STAGES-1 steps in flight; no step is ever loaded twice (short split-K slices
     // would otherwise multiply their traffic)
@@ -180,6 +194,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
                     af[i] = *reinterpret_cast<const bf16x8_t*>(as + (i * 16 + frow) * ROWB + coff);
+                if constexpr (EPI == EPI_GELU_LN) {  // row statistics of the raw A rows (LN folded in)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const float f = bf16_to_f32((bf16_t)af[i][e]);
+                            ln_s1[i] += f;
+                            ln_s2[i] = fmaf(f, f, ln_s2[i]);
+                        }
+                }
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     bfr[j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frow) * ROWB + coff);
@@ -194,6 +218,27 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
         }
     }
     wait_vmcnt<0>();  // drain the tail DMA before the workgroup may exit / LDS be reused
+
+    if constexpr (EPI == EPI_GELU_LN) {
+        // lanes frow, frow + 16, frow + 32, frow + 48 hold the 4 k-chunks of the same row
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            ln_s1[i] += __shfl_xor(ln_s1[i], 16);
+            ln_s2[i] += __shfl_xor(ln_s2[i], 16);
+            ln_s1[i] += __shfl_xor(ln_s1[i], 32);
+            ln_s2[i] += __shfl_xor(ln_s2[i], 32);
+        }
+        if (wn == 0 && lane < 16) {
+            const float invk = 1.0f / (float)K;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const float mean = ln_s1[i] * invk;
+                const float var = fmaxf(ln_s2[i] * invk - mean * mean, 0.f);
+                ln_stat[wm * WTM + i * 16 + frow] = make_float2(mean, rsqrtf(var + ep.ln_eps));
+            }
+        }
+        // (read after the staged epilogue's first __syncthreads)
+    }
 
     if constexpr (IN == IN_FP8) {  // dequantise: per-row activation scale x per-channel weight scale
         const int rb = m0 + wm * WTM + (lane >> 4) * 4;
@@ -277,7 +322,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
     }
 
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_PARTIAL ||
-                  EPI == EPI_QKV) {
+                  EPI == EPI_QKV || EPI == EPI_GELU_LN) {
         // LDS-staged store: the MFMA layout puts 16 consecutive columns on 16 lanes (2-4 B each), so
         // direct stores write 32-64 B pieces; staging the tile through LDS (padded rows: the four
         // lane groups' rows land 64 B apart, conflict-free) turns the write-out into full 16-B-per-lane
@@ -288,14 +333,24 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
         __syncthreads();                   // every wave is done reading the last ring stage
         const int lrow0 = wm * WTM + (lane >> 4) * 4;
         const int lcol0 = wn * WTN + (lane & 15);
+        float2 st[TM][4];
+        if constexpr (EPI == EPI_GELU_LN) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) st[i][r] = ln_stat[lrow0 + i * 16 + r];
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const float bv = (EPI != EPI_PARTIAL && ep.bias) ? ep.bias[n0 + lcol0 + j * 16] : 0.f;
+            const float c1 = EPI == EPI_GELU_LN ? ep.ln_c1[n0 + lcol0 + j * 16] : 0.f;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = acc[i][j][r] + bv;
+                    if constexpr (EPI == EPI_GELU_LN)
+                        v = gelu_tanh(st[i][r].y * fmaf(-st[i][r].x, c1, acc[i][j][r]) + bv);
                     if constexpr (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
                     if constexpr (EPI == EPI_GELU_ERF) v = gelu_erf(v);
                     char* dst = smem + (lrow0 + i * 16 + r) * SROW + (lcol0 + j * 16) * OB;
@@ -352,9 +407,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
                     reinterpret_cast<bf16_t*>(ep.out)[(size_t)row * ep.ldo + col] = f32_to_bf16(gelu_tanh(v));
                 } else if constexpr (EPI == EPI_GELU_ERF) {
                     reinterpret_cast<bf16_t*>(ep.out)[(size_t)row * ep.ldo + col] = f32_to_bf16(gelu_erf(v));
-                } else if constexpr (EPI == EPI_F32) {
+                } else if constexpr (EPI == EPI_F32 || EPI == EPI_F32X2) {
                     if (ep.resid) v += ep.resid[(size_t)row * ep.ldr + col];
                     reinterpret_cast<float*>(ep.out)[(size_t)row * ep.ldo + col] = v;
+                    if constexpr (EPI == EPI_F32X2) reinterpret_cast<bf16_t*>(ep.out2)[(size_t)row * ep.ldo2 + col] = f32_to_bf16(v);
                 } else if constexpr (EPI == EPI_PARTIAL) {
                     reinterpret_cast<float*>(ep.out)[(size_t)split * ep.split_stride + (size_t)row * ep.ldo + col] =
                         acc[i][j][r];
@@ -383,7 +439,7 @@ static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw
     const int tiles = ((M + BM - 1) / BM) * (N / BN) * (EPI == EPI_PARTIAL ? ep.split_k : 1);
     size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
     const size_t stage_out = (size_t)BM * (BN * (EPI == EPI_PARTIAL ? 4 : 2) + 16);  // LDS-staged epilogue
-    if (EPI != EPI_ARGMAX && EPI != EPI_F32 && stage_out > lds) lds = stage_out;
+    if (EPI != EPI_ARGMAX && EPI != EPI_F32 && EPI != EPI_F32X2 && stage_out > lds) lds = stage_out;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN>),
@@ -501,9 +557,13 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     // tiles' operands (profiles/r3_kern_sweep_m512.jsonl: QKV 9.7 -> 8.5 us, c_fc 10.2 -> 8.7 us,
     // c_proj split-2 10.5 -> split-4 8.5 us); DLMS_GEMM96=0 turns it off (A/B)
     if (gemm96_on() && N % 96 == 0 && M > 256 && M <= 512 && N != 768 &&
-        (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_QKV || (EPI == EPI_PARTIAL && split == 4)) &&
+        (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_LN || EPI == EPI_QKV ||
+         (EPI == EPI_PARTIAL && split == 4)) &&
         (long)((M + 63) / 64) * (N / 96) * split <= 256)
         return launch_gemm_cfg<64, 96, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    // the out-projection feeding a folded LayerNorm (no split-K: the residual is updated in place):
+    // 32x64 tiles, 6-deep ring -> 192 workgroups at M 512, d 768
+    if (EPI == EPI_F32X2 && M > 64 && M <= 512) return launch_gemm_cfg<32, 64, 2, 2, 6, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (EPI == EPI_PARTIAL && gemm96_on() && N == 768 && split == 4 && M > 256 && M <= 512 && K >= 2048)
         return launch_gemm_cfg<64, 96, 2, 2, 4, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
     if (N % 128 == 0 && (t128 >= 1024 || (N >= 8192 && M >= 256)))
@@ -533,6 +593,8 @@ extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, 
         case EPI_QKV: return launch_gemm_epi<EPI_QKV, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
         case EPI_ARGMAX: return launch_gemm_epi<EPI_ARGMAX, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
         case EPI_PARTIAL: return launch_gemm_epi<EPI_PARTIAL, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_F32X2: return launch_gemm_epi<EPI_F32X2, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
+        case EPI_GELU_LN: return launch_gemm_epi<EPI_GELU_LN, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -413,3 +413,45 @@ def test_add_layernorm_fp8_output_and_fp8_argmax():
     top2 = logits.topk(2, dim=1).values
     clear = (top2[:, 0] - top2[:, 1]) > 1e-3  # ignore near-ties (fp32 summation order)
     assert torch.equal(idx[clear], logits.argmax(1)[clear])
+
+
+@pytest.mark.parametrize("M", [37, 256, 512])
+def test_gemm_f32x2_residual_and_bf16_copy(M):
+    """EPI_F32X2 (the out-projection feeding a folded LayerNorm): x += a W^T + b in place, and a bf16
+    copy of the new x, against fp32."""
+    ops = _ops()
+    N, K = 768, 768
+    a, w = _bf(M, K, seed=41), _bf(N, K, scale=0.05, seed=42)
+    bias = torch.randn(N, device=DEV)
+    x = torch.randn(M, N, device=DEV)
+    ref = x + a.float() @ w.float().t() + bias
+    xb = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(a, w, ops.EPI_F32X2, bias=bias, resid=x, out=x, out2=xb)
+    torch.testing.assert_close(x, ref, atol=1e-2, rtol=1e-3)
+    assert torch.equal(xb, x.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(37, 3072, 768), (512, 3072, 768), (256, 4096, 1024)])
+def test_gemm_gelu_with_folded_layernorm(M, N, K):
+    """EPI_GELU_LN: c_fc with LN2 folded in (statistics from the raw bf16 A rows inside the K loop,
+    ops.fold_ln_weights) against fp32 gelu(LN(x) W^T + b) -- including rows with a large mean, where
+    the algebraic form's cancellation would show."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(43)
+    x = torch.randn(M, K, generator=g) * 2.0
+    x[::7] += 25.0  # large-mean rows
+    x = x.to(DEV)
+    gamma = (1.0 + 0.3 * torch.randn(K, generator=g)).to(DEV)
+    beta = (0.2 * torch.randn(K, generator=g)).to(DEV)
+    w = _bf(N, K, scale=0.05, seed=44)
+    b = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    wp, c1, c2 = ops.fold_ln_weights(gamma, beta, w, b)
+    xb = x.to(torch.bfloat16)
+    out = ops.gemm(xb, wp, ops.EPI_GELU_LN, bias=c2, ln_c1=c1, ln_eps=1e-5)
+    xf = xb.float()  # the kernel sees bf16(x): compare against LN of exactly that
+    ln = torch.nn.functional.layer_norm(xf, (K,), gamma, beta, 1e-5)
+    ref = torch.nn.functional.gelu(ln @ w.float().t() + b, approximate="tanh")
+    torch.testing.assert_close(out.float(), ref, atol=4e-2, rtol=3e-2)
+    # and against the unfused path the engine used before (bf16 LN output -> GELU GEMM)
+    unfused = ops.gemm(ln.to(torch.bfloat16), w, ops.EPI_GELU_TANH, bias=b)
+    assert (out.float() - unfused.float()).abs().max().item() < 0.1
