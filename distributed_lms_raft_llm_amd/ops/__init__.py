@@ -1238,6 +1238,13 @@ def gemm_ps_geometry(M: int, N: int, epi: int, split: int = 1, cus: int = 256, K
     kc = K // max(1, split)
     fits4 = 64 * (kc * 2 + 32) + 8 * 4096 <= PS_LDS_BYTES
     mt = 4 if ((epi == EPI_ARGMAX or M >= 512) and fits4) else 2
+    # LM head: 80-row panels (DLMS_PS_MT=5) where they take fewer row blocks (512 rows: 7 passes over
+    # the 77 MB weight instead of 8) and still fit the LDS (K <= 768).  Opt-in: measured 1 % slower
+    # at 1024 queries (704.8 / 707.9 vs 713.3 / 711.0 k tok/s, profiles/r3_sweep_lmhead_mt.jsonl)
+    fits5 = 80 * (kc * 2 + 32) + 8 * 4096 <= PS_LDS_BYTES
+    want = int(os.environ.get("DLMS_PS_MT", "4"))
+    if epi == EPI_ARGMAX and mt == 4 and want == 5 and fits5 and -(-M // 80) < -(-M // 64):
+        mt = 5
     nt = 2
     row_blocks = -(-M // (16 * mt))
     tiles = N // (16 * nt)

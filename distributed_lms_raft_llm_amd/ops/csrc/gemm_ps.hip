@@ -110,7 +110,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
 
     char* stage = smem + BM * row_bytes + wave * PS_STAGE;
 
-    auto finish_tile = [&](int step, unsigned int swl) {
+    auto finish_tile = [&](int step, unsigned int swl, unsigned int swl2) {
         const int tile = slot + (step / nch) * slots;
         const int col0 = tile * NT * 16;  // first column of the tile
         if constexpr (EPI == PS_ARGMAX) {
@@ -120,7 +120,9 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
                 for (int r = 0; r < 4; ++r) {
                     // the tile's (<= 32) columns share one seen-bitmap word per row; lane (g, 4i + r)
                     // loaded the word of row 16i + 4g + r
-                    const unsigned int bits = __shfl(swl, g * 16 + 4 * i + r, 64);
+                    // (row tiles 4.. of an 80-row panel: the second word, swl2)
+                    const unsigned int bits = i < 4 ? __shfl(swl, g * 16 + 4 * i + r, 64)
+                                                    : __shfl(swl2, g * 16 + 4 * (i - 4) + r, 64);
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
                         const int gcol = col0 + 16 * t + fr + ep.col_offset;
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
 
     auto compute = [&](const bf16x8_t (&b)[PS_KBC][NT], int step) {
         const int kb0 = (step % nch) * PS_KBC;
-        unsigned int swl = 0;
+        unsigned int swl = 0, swl2 = 0;
         if constexpr (EPI == PS_ARGMAX) {
             // one seen-bitmap word per lane per chunk (unconditional: a static load count keeps the
             // counted vmcnt of the double-buffered weight stream); its latency hides under the MFMAs
@@ -208,6 +210,12 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
             int srow = m0 + 16 * (fr >> 2) + 4 * g + (fr & 3);
             srow = srow < M ? srow : M - 1;
             swl = ep.seen[(size_t)srow * ep.seen_words + ((tile * NT * 16 + ep.col_offset) >> 5)];
+            if constexpr (MT > 4) {  // a lane's word covers row tiles 0..3; tiles 4..7 take a second one
+                static_assert(MT <= 8, "two seen words per lane cover at most 8 row tiles");
+                int srow2 = m0 + 16 * ((fr >> 2) + 4) + 4 * g + (fr & 3);
+                srow2 = srow2 < M ? srow2 : M - 1;
+                swl2 = ep.seen[(size_t)srow2 * ep.seen_words + ((tile * NT * 16 + ep.col_offset) >> 5)];
+            }
         }
 #pragma unroll
         for (int kb = 0; kb < PS_KBC; ++kb) {
@@ -220,7 +228,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
 #pragma unroll
                 for (int t = 0; t < NT; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[kb][t], acc[i][t], 0, 0, 0);
         }
-        if (step % nch == nch - 1) finish_tile(step, swl);
+        if (step % nch == nch - 1) finish_tile(step, swl, swl2);
     };
 
     // register ring of weight chunks: NBUF-1 chunks in flight behind the one being computed.  The
@@ -309,6 +317,7 @@ extern "C" hipError_t dlms_gemm_ps(int epi, const void* A, int lda, const void* 
     if (mt == 2 && nt == 2) return launch_ps<E, 2, 2>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
     if (mt == 4 && nt == 1) return launch_ps<E, 4, 1>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
     if (mt == 4 && nt == 2) return launch_ps<E, 4, 2>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
+    if (E == PS_ARGMAX && mt == 5 && nt == 2) return launch_ps<PS_ARGMAX, 5, 2>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
     return hipErrorInvalidValue;
     switch (epi) {
         case PS_BF16: PS_GEO(PS_BF16)

@@ -531,7 +531,7 @@ __device__ __forceinline__ void addln_rows_lds(const void* __restrict__ x_in, fl
 }
 
 template <int EPI, int NSPLIT, int NV4, int RPW, int KBW, bool XFIX>
-__global__ __launch_bounds__(256) void skinny_addln_kernel(const void* __restrict__ x_in, float* __restrict__ x_out,
+__device__ __forceinline__ void skinny_addln_impl(const void* __restrict__ x_in, float* __restrict__ x_out,
                                                          int ldx, const float* __restrict__ parts, int ldp,
                                                          long long split_stride, const float* __restrict__ res_bias,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -579,6 +579,18 @@ __global__ __launch_bounds__(256) void skinny_addln_kernel(const void* __restric
 #pragma unroll
     for (int s = 1; s < NW; ++s) acc[0] += *reinterpret_cast<const f32x4_t*>(red + ((size_t)s * 64 + lane) * 4);
     skinny_store<EPI, 1>(acc, M, ng * 16 + fr, g, ep);
+}
+
+template <int EPI, int NSPLIT, int NV4, int RPW, int KBW, bool XFIX>
+__global__ __launch_bounds__(256) void skinny_addln_kernel(const void* __restrict__ x_in, float* __restrict__ x_out,
+                                                         int ldx, const float* __restrict__ parts, int ldp,
+                                                         long long split_stride, const float* __restrict__ res_bias,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         float eps, const bf16_t* __restrict__ Wsh, int M, int N, int K,
+                                                         GemmEpi ep, uint4* __restrict__ zero_buf, int zero_chunks,
+                                                         long long xcs) {
+    skinny_addln_impl<EPI, NSPLIT, NV4, RPW, KBW, XFIX>(x_in, x_out, ldx, parts, ldp, split_stride, res_bias, gamma,
+                                                        beta, eps, Wsh, M, N, K, ep, zero_buf, zero_chunks, xcs);
 }
 
 // launch arguments shared by every instantiation of the fused add+LN kernels

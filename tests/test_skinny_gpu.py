@@ -531,8 +531,9 @@ def test_gemm_ps_qkv(M):
     torch.testing.assert_close(vs, z[:, 2 * D:], atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,K", [(3, 768), (64, 768), (512, 768), (512, 1024), (1024, 1024), (256, 1280)])
-def test_gemm_ps_argmax_matches_tiled(M, K):
+@pytest.mark.parametrize("M,K,mt", [(3, 768, 0), (64, 768, 0), (300, 768, 5), (512, 768, 0), (512, 768, 5),
+                                    (512, 1024, 0), (1024, 1024, 0), (256, 1280, 0)])
+def test_gemm_ps_argmax_matches_tiled(M, K, mt):
     """Same keys as the tiled LM head's fused penalty + argmax (identical per-element sums are not
     required: compare the decoded token wherever the fp32 top-2 margin is clear); K > 1008 (GPT-2
     medium and wider) takes 32-row panels so the panel fits in LDS."""
@@ -544,8 +545,12 @@ def test_gemm_ps_argmax_matches_tiled(M, K):
     seen = torch.randint(-2**31, 2**31 - 1, (M, Vp // 32), generator=torch.Generator().manual_seed(3),
                          dtype=torch.int64).to(torch.int32).to(DEV)
     seen &= 0x01010101  # ~1/8 of the vocabulary penalised
-    keys = torch.zeros(M, ops.gemm_ps_key_slots(M, Vp, K), dtype=torch.int64, device=DEV)
-    ops.gemm_ps(h, ops.shuffle_weight(w), ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2)
+    geo = ops.gemm_ps_geometry(M, Vp, ops.EPI_ARGMAX, K=K)
+    if mt:  # the 80-row panel (two seen-bitmap words per lane), not the default
+        geo = (mt, geo[1], max(1, 256 // -(-M // (16 * mt))))
+    keys = torch.zeros(M, 8 * geo[2], dtype=torch.int64, device=DEV)
+    ops.gemm_ps(h, ops.shuffle_weight(w), ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2,
+                geometry=geo)
     tok = ops.argmax_reduce(keys)
     got = ((~(tok & 0xFFFFFFFF)) & 0xFFFFFFFF).cpu()
     logits = h.float() @ w.float().t()
