@@ -341,10 +341,16 @@ class HipGPT2Engine:
         if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
             # (the latency path's skinny LM head reads the same pre-shuffled copy)
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
-        # batch 1-2 (TP=1, bf16): the persistent dataflow decode -- one launch per chunk of decode
-        # steps (ops/dataflow.py); built on first use (it packs a per-CU copy of the weights)
-        self.dataflow = (os.environ.get("DLMS_DATAFLOW", "0") != "0" and tp_group is None and
-                         not self.w.fp8 and self._df_supported())
+        # batch 1 (TP=1, bf16): the persistent dataflow decode -- one launch per chunk of decode steps
+        # (ops/dataflow.py); built on first use (it packs a per-CU copy of the weights).  Default ON
+        # for GPT-2-124M at one row, where it measured 29.9-30.3 vs 31.6 ms per query launch-per-op
+        # (profiles/r3_df_sweep_grid200.jsonl); at two rows it is slower (58.9 vs 34.9 ms,
+        # r3_df_sweep_fine.jsonl).  DLMS_DATAFLOW=1 forces it on for every supported width,
+        # DLMS_DATAFLOW_ROWS (1 or 2) the row counts it serves, DLMS_DATAFLOW=0 turns it off.
+        df_env = os.environ.get("DLMS_DATAFLOW", "auto")
+        self.dataflow_rows = max(1, min(2, int(os.environ.get("DLMS_DATAFLOW_ROWS", "1"))))
+        self.dataflow = (df_env != "0" and tp_group is None and not self.w.fp8 and
+                         (df_env == "1" or cfg.n_embd == 768) and self._df_supported())
         self._df = None
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
@@ -754,7 +760,8 @@ class HipGPT2Engine:
         from ..ops.dataflow import MAX_ROWS
 
         # (the launch-per-op path serves row counts whose stream window outgrows the LDS ring)
-        return self.dataflow and 1 <= B <= min(MAX_ROWS, self.max_batch) and self._df_decoder().fits(B)
+        return (self.dataflow and 1 <= B <= min(MAX_ROWS, self.max_batch, self.dataflow_rows)
+                and self._df_decoder().fits(B))
 
     def _df_decoder(self):
         if self._df is None:

@@ -206,8 +206,13 @@ class DataflowDecoder:
         self.eng = eng
         cfg, dev = eng.cfg, eng.device
         props = torch.cuda.get_device_properties(dev)
-        G = grid or int(os.environ.get("DLMS_DF_GRID", "0")) or min(int(props.multi_processor_count), 256)
-        gs = gs or int(os.environ.get("DLMS_DF_GS", "4"))
+        # 200 of 256 CUs, 2 CUs per head's attention: batch 1 on one box 29.9-30.3 ms against 33.7 at
+        # the full grid with 4 per head and 31.6 launch-per-op (profiles/r3_df_sweep_grid200.jsonl,
+        # r3_df_sweep_grid_gs.jsonl): fewer contributors per counted residual word shorten the
+        # all-to-all edges more than the extra rows per CU lengthen the phases
+        cus = int(props.multi_processor_count)
+        G = grid or int(os.environ.get("DLMS_DF_GRID", "0")) or min(cus * 25 // 32, 256)
+        gs = gs or int(os.environ.get("DLMS_DF_GS", "2"))
         while cfg.n_head * gs > G and gs > 1:
             gs //= 2
         self.G, self.GS = G, gs

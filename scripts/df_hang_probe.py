@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     os.environ["DLMS_DATAFLOW"] = "1"
+    os.environ["DLMS_DATAFLOW_ROWS"] = "2"
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
     from distributed_lms_raft_llm_amd.models.config import gpt2_config
     from distributed_lms_raft_llm_amd.models.gpt2 import init_gpt2_weights

@@ -17,6 +17,7 @@ def engine(cfg, w, df: bool, **kw):
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
     os.environ["DLMS_DATAFLOW"] = "1" if df else "0"
+    os.environ["DLMS_DATAFLOW_ROWS"] = "2"
     return HipGPT2Engine(cfg, w, **kw)
 
 

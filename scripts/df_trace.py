@@ -29,6 +29,7 @@ def main():
 
     cfg = gpt2_config(args.model)
     os.environ["DLMS_DATAFLOW"] = "1"
+    os.environ["DLMS_DATAFLOW_ROWS"] = "2"
     eng = HipGPT2Engine(cfg, init_gpt2_weights(cfg, seed=0), max_batch=2, max_length=150)
     g = torch.Generator().manual_seed(1)
     prompts = torch.randint(0, cfg.vocab_size - 1, (args.batch, 32), generator=g).tolist()

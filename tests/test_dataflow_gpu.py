@@ -34,15 +34,17 @@ def _prompts(cfg, lens, seed=1):
 def _engine(cfg, w, dataflow: bool, **kw):
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
-    old = os.environ.get("DLMS_DATAFLOW")
+    saved = {k: os.environ.get(k) for k in ("DLMS_DATAFLOW", "DLMS_DATAFLOW_ROWS")}
     os.environ["DLMS_DATAFLOW"] = "1" if dataflow else "0"
+    os.environ["DLMS_DATAFLOW_ROWS"] = "2"  # both row counts (the default serves one)
     try:
         return HipGPT2Engine(cfg, w, **kw)
     finally:
-        if old is None:
-            del os.environ["DLMS_DATAFLOW"]
-        else:
-            os.environ["DLMS_DATAFLOW"] = old
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 def _oracle(cfg, w, outs, prompts, eps=0.05):
