@@ -343,14 +343,15 @@ class HipGPT2Engine:
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
         # batch 1 (TP=1, bf16): the persistent dataflow decode -- one launch per chunk of decode steps
         # (ops/dataflow.py); built on first use (it packs a per-CU copy of the weights).  Default ON
-        # for GPT-2-124M at one row, where it measured 29.9-30.3 vs 31.6 ms per query launch-per-op
-        # (profiles/r3_df_sweep_grid200.jsonl); at two rows it is slower (58.9 vs 34.9 ms,
+        # at one row for the widths where it was measured faster: GPT-2-124M 29.9-30.3 vs 31.6 ms per
+        # query launch-per-op (profiles/r3_df_sweep_grid200.jsonl), GPT-2-medium 73.5 vs 76.9 ms
+        # (r3_df_medium_b1.jsonl, same tokens); at two rows it is slower (58.9 vs 34.9 ms,
         # r3_df_sweep_fine.jsonl).  DLMS_DATAFLOW=1 forces it on for every supported width,
         # DLMS_DATAFLOW_ROWS (1 or 2) the row counts it serves, DLMS_DATAFLOW=0 turns it off.
         df_env = os.environ.get("DLMS_DATAFLOW", "auto")
         self.dataflow_rows = max(1, min(2, int(os.environ.get("DLMS_DATAFLOW_ROWS", "1"))))
         self.dataflow = (df_env != "0" and tp_group is None and not self.w.fp8 and
-                         (df_env == "1" or cfg.n_embd == 768) and self._df_supported())
+                         (df_env == "1" or cfg.n_embd in (768, 1024)) and self._df_supported())
         self._df = None
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
