@@ -47,12 +47,18 @@
 namespace df {
 
 constexpr int NC = 4;                 // compute waves
-constexpr int NL = 2;                 // loader waves
+#ifndef DF_NL
+#define DF_NL 2
+#endif
+#ifndef DF_INFL
+#define DF_INFL 48
+#endif
+constexpr int NL = DF_NL;             // loader waves (A/B builds: -DDF_NL=3)
 constexpr int NWAVES = NC + NL + 1;   // + comm
 constexpr int NTHREADS = 64 * NWAVES;
 constexpr int SHARDS = 8;             // arrival counters are sharded by blockIdx % 8
 constexpr int CSTRIDE = 16;           // u64 words between shards (one 128-B line each)
-constexpr int INFL = 48;              // LDS-DMA units (1 KiB) in flight per loader wave
+constexpr int INFL = DF_INFL;         // LDS-DMA units (1 KiB) in flight per loader wave (<= 71: vmcnt is 6 bits)
 #ifndef DF_COPIES
 #define DF_COPIES 2
 #endif
@@ -734,7 +740,7 @@ __device__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& l
         }
         ++k;
         if (k * LB >= (unsigned)INFL) {
-            asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // INFL - LB units may stay in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFL - LB) : "memory");  // INFL - LB units may stay in flight
             const unsigned done = k - (INFL - LB) / LB;
             if (done > published) {
                 published = done;
