@@ -23,6 +23,7 @@ No host round trip happens inside a step; the host only checks the stop flags ev
 from __future__ import annotations
 
 import itertools
+import logging
 import math
 import os
 import time
@@ -33,7 +34,10 @@ import torch
 
 from .. import ops
 from ..models.config import GPT2Config
+from ..utils.metrics import METRICS
 from .weights import GPT2DeviceWeights, prepare_gpt2_weights
+
+log = logging.getLogger(__name__)
 
 
 @dataclass
@@ -353,6 +357,9 @@ class HipGPT2Engine:
         self.dataflow = (df_env != "0" and tp_group is None and not self.w.fp8 and
                          (df_env == "1" or cfg.n_embd in (768, 1024)) and self._df_supported())
         self._df = None
+        self._df_status = None  # the last decode() launch's error words in flight (dataflow_status_async)
+        self._df_off_until = 0.0  # after an aborted launch: launch-per-op until then (DLMS_DF_COOLDOWN_S)
+        self.df_aborts = 0
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -762,7 +769,47 @@ class HipGPT2Engine:
 
         # (the launch-per-op path serves row counts whose stream window outgrows the LDS ring)
         return (self.dataflow and 1 <= B <= min(MAX_ROWS, self.max_batch, self.dataflow_rows)
-                and self._df_decoder().fits(B))
+                and time.monotonic() >= self._df_off_until and self._df_decoder().fits(B))
+
+    def _df_run(self, B: int, steps: int, penalty: float) -> bool:
+        """Launch the dataflow decode for ``steps`` steps of rows [0, B); False (nothing ran) when
+        the device cannot hold its grid at once -- the dataflow path is then off for good."""
+        from ..ops.dataflow import DataflowUnavailable
+
+        try:
+            self._df_decoder().run(B, steps, penalty)
+        except DataflowUnavailable as e:
+            log.warning("%s: serving launch-per-op", e)
+            self.dataflow = False
+            return False
+        return True
+
+    def _df_note(self, st):
+        """An aborted dataflow launch (error words ``st``): count it and serve launch-per-op for
+        DLMS_DF_COOLDOWN_S seconds (default 30).  Nothing to repair: an aborted launch commits no
+        row state (ops/csrc/dataflow.hip, commit), so whatever runs next redoes those steps."""
+        from ..ops.dataflow import DataflowDecoder
+
+        self.df_aborts += 1
+        METRICS.inc("engine_dataflow_aborts")
+        self._df_off_until = time.monotonic() + float(os.environ.get("DLMS_DF_COOLDOWN_S", "30"))
+        log.warning("%s (committed %d steps); launch-per-op for a while", DataflowDecoder.describe(st), st[4])
+
+    def dataflow_status_async(self) -> "HostResult | None":
+        """Whether the last ``decode()`` chunk ran the dataflow kernel and it ABORTED before
+        committing (``.result()`` True: that chunk made no progress, the row state is unchanged);
+        None if the chunk ran launch-per-op.  A copy in flight, like ``flags_async``."""
+        h, self._df_status = self._df_status, None
+        if h is None:
+            return None
+
+        def finish():
+            st = h.result()
+            if st[0]:
+                self._df_note(st)
+            return bool(st[0]) and not st[4]
+
+        return HostResult(finish)
 
     def _df_decoder(self):
         if self._df is None:
@@ -1149,8 +1196,9 @@ class HipGPT2Engine:
         """``steps`` greedy decode steps over slots [0, B) (finished/inert slots are no-ops)."""
         if B > self.max_batch or B not in (_bucket(B), self.max_batch):
             raise ValueError(f"decode: batch bucket {B} invalid")
-        if steps > 0 and self._df_ok(B):
-            self._df_decoder().run(B, steps, repetition_penalty)
+        self._df_status = None
+        if steps > 0 and self._df_ok(B) and self._df_run(B, steps, repetition_penalty):
+            self._df_status = self._df.status_async()
             return
         graph = self._graph_for(B, repetition_penalty) if self.use_graph else None
         kg = self._steps_per_graph_for(B) if graph is not None else 1
@@ -1242,25 +1290,28 @@ class HipGPT2Engine:
         self._prefill(prompts, B, repetition_penalty)
         ev1.record()
         steps_max = T - min(len(p) for p in prompts) - 1
-        if steps_max > 0 and self._df_ok(B):
+        if steps_max > 0 and self._df_ok(B) and self._df_run(B, steps_max, repetition_penalty):
             # one persistent launch for every decode step (it stops on device once all rows finish)
-            df = self._df_decoder()
-            df.run(B, steps_max, repetition_penalty)
             ev2.record()
-            lens = self.lens[:n].cpu().tolist()
-            toks = self.out_tokens[:n].cpu().numpy()
-            df.check()
-            res = [toks[b, : lens[b]].tolist() for b in range(n)]
-            if stats is not None:
-                ev2.synchronize()
-                stats.batch += n
-                stats.prompt_tokens += sum(len(p) for p in prompts)
-                stats.new_tokens += sum(lens[b] - len(prompts[b]) for b in range(n))
-                stats.prefill_ms += ev0.elapsed_time(ev1)
-                stats.decode_ms += ev1.elapsed_time(ev2)
-                stats.steps += steps_max
-                stats.graph = False
-            return res
+            st = tuple(self._df.err[:5].cpu().tolist())
+            if st[0]:
+                self._df_note(st)
+            if st[4]:  # committed (an error after the commit -- a straggler CU -- changes nothing)
+                lens = self.lens[:n].cpu().tolist()
+                toks = self.out_tokens[:n].cpu().numpy()
+                res = [toks[b, : lens[b]].tolist() for b in range(n)]
+                if stats is not None:
+                    ev2.synchronize()
+                    stats.batch += n
+                    stats.prompt_tokens += sum(len(p) for p in prompts)
+                    stats.new_tokens += sum(lens[b] - len(prompts[b]) for b in range(n))
+                    stats.prefill_ms += ev0.elapsed_time(ev1)
+                    stats.decode_ms += ev1.elapsed_time(ev2)
+                    stats.steps += st[4]
+                    stats.graph = False
+                return res
+            # aborted before its commit: the rows are exactly as the prefill left them -- decode
+            # them launch-per-op below
         graph = self._graph_for(B, repetition_penalty) if (self.use_graph and steps_max > 0) else None
         kg = self._steps_per_graph_for(B)
         if graph is None or self.check_every % kg:

@@ -58,6 +58,11 @@ def health_async(eng):
     return f() if f is not None else None
 
 
+def dataflow_status_async(eng):
+    f = getattr(eng, "dataflow_status_async", None)
+    return f() if f is not None else None
+
+
 class PeerStalled(RuntimeError):
     """A tensor-parallel peer never reached a collective: the affected chunk's tokens are garbage."""
 
@@ -173,7 +178,12 @@ class ContinuousBatcher:
                     return
                 admits: list[tuple[int, _Req]] = []
                 while self._queue and self._free and len(admits) < self.max_admit:
-                    admits.append((heapq.heappop(self._free), self._queue.popleft()))
+                    r = self._queue.popleft()
+                    # RUNNING from here on: a caller's cancel() (a gRPC deadline, asyncio.wait_for
+                    # timing out on a wrap_future) can no longer race the result; a request
+                    # cancelled while it queued is dropped
+                    if r.future.set_running_or_notify_cancel():
+                        admits.append((heapq.heappop(self._free), r))
             if admits:
                 ta = time.perf_counter()
                 with roctx_range("prefill"):
@@ -201,7 +211,8 @@ class ContinuousBatcher:
                 td = time.perf_counter()
                 with roctx_range("decode_chunk"):
                     eng.decode(B, steps, self.penalty)
-                    cur = (flags_async(eng, B), dict(self._active), health_async(eng))
+                    cur = (flags_async(eng, B), dict(self._active), health_async(eng), dataflow_status_async(eng),
+                           steps)
                 for r in self._active.values():
                     r.steps_left = max(0, r.steps_left - steps)
                 self.steps += steps
@@ -216,6 +227,14 @@ class ContinuousBatcher:
                     # fail every live request (the _run handler) rather than return wrong tokens
                     METRICS.inc(f"{self.name}_peer_stalls")
                     raise PeerStalled("a tensor-parallel peer timed out in an xGMI collective")
+                if prev[3] is not None and prev[3].result():
+                    # the persistent dataflow kernel aborted that chunk before committing anything:
+                    # no row advanced (the engine serves launch-per-op for a while); give the
+                    # requests their step budget back so later chunks are not cut short
+                    METRICS.inc(f"{self.name}_dataflow_aborts")
+                    for s, r in prev[1].items():
+                        if self._active.get(s) is r:
+                            r.steps_left += prev[4]
                 # by identity: a slot retired one chunk earlier may already hold a new request
                 done = [s for s, r in prev[1].items() if s < len(flags) and flags[s] and self._active.get(s) is r]
                 if done:
@@ -239,4 +258,5 @@ class ContinuousBatcher:
             if n_new > 1:  # time per output token after the first
                 METRICS.observe(f"{self.name}_tpot_ms", (now - r.t_first) * 1e3 / (n_new - 1))
             METRICS.inc(f"{self.name}_tokens", n_new)
-            r.future.set_result(out)
+            if not r.future.done():
+                r.future.set_result(out)

@@ -134,9 +134,20 @@ class BlobStore:
 
     def put_bytes(self, data: bytes) -> str:
         sha = hashlib.sha256(data).hexdigest()
-        if not self.has(sha):
+        if not self._touch(sha):
             self.put_chunks(sha, [data])
         return sha
+
+    def _touch(self, sha: str) -> bool:
+        """Refresh an existing object's mtime (False if absent): an upload of content that is
+        already here counts as a fresh upload for the GC's grace period -- otherwise a stale
+        unreferenced object re-uploaded just before a GC pass could be deleted under a PutBlob
+        that is about to commit a reference to it."""
+        try:
+            os.utime(self.cas_path(sha))
+            return True
+        except FileNotFoundError:
+            return False
 
     def get_sha(self, sha: str, relpath: str | None = None, fetch_timeout: float = 30.0) -> bytes:
         """Bytes of CAS object ``sha`` (an entry's own upload: two same-named uploads keep their
@@ -152,22 +163,29 @@ class BlobStore:
                         break
         return self.get(relpath, sha) if relpath else b""
 
-    def gc(self, referenced: set[str], grace_s: float = 600.0) -> int:
+    def gc(self, referenced: set[str], grace_s: float = 600.0, still_referenced=None) -> int:
         """Delete CAS objects no replicated entry references any more (snapshot time).  Objects
         younger than ``grace_s`` survive: a pre-replicated upload whose PutBlob has not committed
-        yet is unreferenced but live.  ``uploads/<name>`` links keep their own inode.  Returns the
-        number of objects removed."""
+        yet is unreferenced but live (re-uploads refresh the mtime, ``_touch``).  Each candidate
+        is re-checked right before its unlink -- its mtime read again, and ``still_referenced(sha)``
+        (the live state, not the snapshot-time set) asked -- since the scan runs in the
+        background while entries keep committing.  ``uploads/<name>`` links keep their own inode.
+        Returns the number of objects removed."""
         d = os.path.join(self.root, CAS_FOLDER)
-        now = time.time()
         removed = 0
         for name in os.listdir(d):
             if not is_sha256(name) or name in referenced:
                 continue
             path = os.path.join(d, name)
             try:
-                if now - os.path.getmtime(path) >= grace_s:
-                    os.unlink(path)
-                    removed += 1
+                if time.time() - os.path.getmtime(path) < grace_s:
+                    continue
+                if still_referenced is not None and still_referenced(name):
+                    continue
+                if time.time() - os.path.getmtime(path) < grace_s:  # touched meanwhile
+                    continue
+                os.unlink(path)
+                removed += 1
             except FileNotFoundError:
                 pass
         return removed
@@ -186,7 +204,7 @@ class BlobStore:
         replica acknowledges a pre-replication push only then, so "a majority holds the blob"
         survives a crash just like the log entry that depends on it."""
         path = self.cas_path(sha)
-        if os.path.exists(path):
+        if self._touch(sha):
             for _ in chunks:  # drain the stream
                 pass
             return True

@@ -192,6 +192,8 @@ def _bind(L):
         raise RuntimeError("XgmiArgs ABI mismatch between ctypes mirror and compiled library")
     L.dlms_gemm_force_tile.argtypes = [ctypes.c_int]
     L.dlms_gemm_force_tile.restype = None
+    L.dlms_gemm_tile_count.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.dlms_gemm_tile_count.restype = ctypes.c_long
     L.dlms_attention_variant.argtypes = [ctypes.c_int]
     L.dlms_attention_variant.restype = None
     # in-situ tuning knobs (tests and production leave them unset)
@@ -251,6 +253,16 @@ def raise_on_device_errors():
 def available() -> bool:
     """True when a GPU is present (the HIP library will then be required, not optional)."""
     return torch.cuda.is_available()
+
+
+def gemm_tile_count(bm: int, bn: int) -> int:
+    """Launches of the tiled GEMM issued so far with a ``bm`` x ``bn`` tile (host-side census;
+    ``gemm_tile_reset()`` zeroes it): tests assert which instantiation a decode path dispatches."""
+    return int(lib().dlms_gemm_tile_count(bm, bn))
+
+
+def gemm_tile_reset():
+    lib().dlms_gemm_tile_count(-1, -1)
 
 
 def _check(err: int, what: str):

@@ -112,6 +112,8 @@ struct Args {
     long long step_words;
     int R, D, H, L, V, T, seen_words, eos, nsteps, A, C, max_nq, swl, ring_bytes, ldx, n_slots, P, nt_weights;
     int ko, kf;  // K (padded to 16) of the per-CU W_o block and c_proj block
+    int fault_step;  // test hook: >= 0 makes the last CU abort at that step as a timed-out wait would
+    int coop;        // launch cooperatively (co-residency guaranteed by the runtime)
     int exp_att[8], exp_mlp[8];  // contributions each residual copy receives (attention / MLP CUs)
     float eps, penalty;
 };
@@ -147,8 +149,8 @@ enum { C_READY = 0, C_ABORT = 2, C_DONE = 3, C_CONT = 4, C_LOADED = 8, C_PHDONE 
 // (C_LOADED + j: loader wave j's completed-batch count)
 // row state words (st[b * 8 + k])
 enum { S_TOK = 0, S_POS = 1, S_FIN = 2, S_LEN = 3, S_SLOT = 4 };
-// error codes
-enum { E_WAIT_CNT = 1, E_WAIT_GRAN = 2, E_WAIT_LDS = 3, E_LOADER = 4 };
+// error codes (err[0]); err[4] = 1 + steps run once CU 0 has committed the row state
+enum { E_WAIT_CNT = 1, E_WAIT_GRAN = 2, E_WAIT_LDS = 3, E_LOADER = 4, E_INJECTED = 5 };
 
 // scratch word offsets (per step)
 struct Scr {
@@ -407,11 +409,12 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
     const int D3 = 3 * D;
 
     // ---- row state
-    int tok[R], pos[R], fin[R], len[R], slot[R];
+    int tok[R], pos[R], fin[R], len[R], slot[R], len0[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         slot[r] = a.slots[r];
         len[r] = a.lens[slot[r]];
+        len0[r] = len[r];
         fin[r] = a.finished[slot[r]];
         tok[r] = a.cur_tok[slot[r]];
         pos[r] = a.cur_pos[slot[r]];
@@ -444,6 +447,12 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
         i64 xs[R][EPL];  // this CU's copy of the residual stream (int64 fixed point)
         for (int l = 0; l < L && ok; ++l) {
             const Layer lw = a.layers[l];
+            if (s == a.fault_step && l == L - 1 && blockIdx.x == G - 1) {  // test hook: an aborted hand-off
+                set_err(a, E_INJECTED, 10 * l, s);
+                lds_st(ctl + C_ABORT, 1u);
+                ok = false;
+                break;
+            }
             stamp(a, s, l, 0, lane);
             if (l == 0) {
                 stamp_val(a, s, 0, 26, __builtin_amdgcn_s_memtime());
@@ -632,11 +641,10 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
                 int t = best ? (int)(~(unsigned)(best & 0xffffffffull)) : a.eos;
                 t = (t >= 0 && t < a.V) ? t : a.eos;
                 if (blockIdx.x == 0 && lane == 0) a.out_tokens[(size_t)slot[r] * T + live_len] = t;
+                // (this CU's LDS slice only: the global bitmap is updated at the commit, so an
+                // aborted launch leaves every piece of row state as it found it)
                 const int rel = t - cu.v0;
-                if (rel >= 0 && rel < cu.nv && lane == 0) {
-                    seen[r * a.swl + (rel >> 5)] |= 1u << (rel & 31);
-                    atomicOr(a.seen + (size_t)slot[r] * a.seen_words + (t >> 5), 1u << (t & 31));
-                }
+                if (rel >= 0 && rel < cu.nv && lane == 0) seen[r * a.swl + (rel >> 5)] |= 1u << (rel & 31);
                 len[r] = live_len + 1;
                 if (t == a.eos || live_len + 1 >= T) fin[r] = 1;
                 tok[r] = t;
@@ -655,10 +663,19 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
         lds_st(ctl + C_READY, pid_of(s, L, 1, L));
         if (!cont) break;
     }
-    // ---- write the row state back (CU 0): decode_update's outputs, incl. the next embedding
+    // ---- commit (CU 0, only if it ran every step it started): decode_update's outputs incl. the
+    // next embedding, and the generated tokens into the global penalty bitmap.  CU 0 passed every
+    // step's argmax counter, so each token it holds saw all G CUs' keys; an aborted launch commits
+    // nothing (the K/V rows and out_tokens entries it wrote lie beyond the committed lengths and
+    // are rewritten by whatever runs these steps again).
     if (ok && blockIdx.x == 0) {
+        drain();  // this wave's out_tokens stores, read back below
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            for (int i = lane; i < len[r] - len0[r]; i += 64) {
+                const int t = (int)gld32(reinterpret_cast<const unsigned*>(a.out_tokens + (size_t)slot[r] * T + len0[r] + i));
+                atomicOr(a.seen + (size_t)slot[r] * a.seen_words + (t >> 5), 1u << (t & 31));
+            }
             if (lane == 0) {
                 a.lens[slot[r]] = len[r];
                 a.finished[slot[r]] = fin[r];
@@ -674,6 +691,10 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
                         bf16_to_f32(a.wte[(size_t)tok[r] * D + e]) + bf16_to_f32(a.wpe[(size_t)pos[r] * D + e]);
                 }
             }
+        }
+        if (lane == 0) {
+            drain();
+            __hip_atomic_store(a.err + 4, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     lds_st(ctl + C_DONE, 1u);
@@ -1255,18 +1276,37 @@ extern "C" long long dlms_df_step_words(int R, int D, int L, int C) { return df:
 extern "C" int dlms_df_threads() { return df::NTHREADS; }
 extern "C" int dlms_df_copies() { return df::COPIES; }
 
+// Every workgroup spins on the others, so the whole grid must be resident at once.  The launcher
+// checks that the device can hold it (occupancy x CUs >= grid; -2 = "cannot", the host then serves
+// the launch-per-op path) and by default launches cooperatively, which makes the runtime guarantee
+// co-residency against other work on the device as well; the bounded waits + commit-only row
+// state are the last line (an aborted launch changes nothing the next launch reads).
+constexpr int DF_NOT_RESIDENT = -2;
 template <int D, int R, int PFG>
-static hipError_t df_launch(const df::Args& a, int grid, int lds, hipStream_t stream) {
+static int df_launch(df::Args a, int grid, int lds, hipStream_t stream) {
     auto k = &df::dataflow_decode_kernel<D, R, PFG>;
-    static bool attr = false;
-    if (!attr) {
+    static int fits_grid = -1;  // the most workgroups the device holds at once (per instantiation)
+    if (fits_grid < 0) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            df::LDS_MAX);
-        if (e != hipSuccess) return e;
-        attr = true;
+        if (e != hipSuccess) return (int)e;
+        int dev = 0, cus = 0, per_cu = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return (int)e;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return (int)e;
+        // (occupancy at the largest LDS any launch of this instantiation asks for)
+        if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k), df::NTHREADS,
+                                                              df::LDS_MAX)) != hipSuccess)
+            return (int)e;
+        fits_grid = per_cu * cus;
+    }
+    if (grid > fits_grid) return DF_NOT_RESIDENT;
+    if (a.coop) {
+        void* params[] = {&a};
+        return (int)hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), dim3(grid), dim3(df::NTHREADS), params,
+                                               (unsigned)lds, stream);
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(df::NTHREADS), lds, stream, a);
-    return hipGetLastError();
+    return (int)hipGetLastError();
 }
 
 extern "C" int dlms_dataflow_decode(const df::Args* args, int grid, hipStream_t stream) {
@@ -1276,8 +1316,8 @@ extern "C" int dlms_dataflow_decode(const df::Args* args, int grid, hipStream_t 
         a.H * 64 != a.D || a.max_nq > 64 || a.ko % 16 || a.kf % 16 || a.ko > 64 || a.kf > 64 || a.kf < 16 || a.nsteps <= 0 || a.C != df::COPIES || a.A < 1 || a.A > grid)
         return (int)hipErrorInvalidValue;
 #define DF_CASE(DD)                                                                           \
-    if (a.D == DD) return (int)(a.R == 1 ? df_launch<DD, 1, 5>(a, grid, lds, stream)           \
-                                         : df_launch<DD, 2, 3>(a, grid, lds, stream));
+    if (a.D == DD) return a.R == 1 ? df_launch<DD, 1, 5>(a, grid, lds, stream)                 \
+                                   : df_launch<DD, 2, 3>(a, grid, lds, stream);
     DF_CASE(128)
     DF_CASE(256)
     DF_CASE(768)

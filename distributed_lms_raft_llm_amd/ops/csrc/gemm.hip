@@ -33,6 +33,7 @@
 //                   no atomics) -- the decode projections with N = d are split 2-4 ways so the
 //                   latency-bound skinny GEMMs put enough workgroups on the 256 CUs.
 #include "common.h"
+#include <atomic>
 #include <stdlib.h>
 
 enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6,
@@ -433,9 +434,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
     }
 }
 
+// host-side launch census by tile shape (tests assert which instantiation a path dispatches;
+// counted when the launch is issued, so graph captures count once per capture)
+static std::atomic<long> g_tile_count[4][4];  // [BM 32/64/128/256][BN 64/96/128/256]
+
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN>
 static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
+    g_tile_count[BM <= 32 ? 0 : BM <= 64 ? 1 : BM <= 128 ? 2 : 3][BN <= 64 ? 0 : BN <= 96 ? 1 : BN <= 128 ? 2 : 3]
+        .fetch_add(1, std::memory_order_relaxed);
     const int tiles = ((M + BM - 1) / BM) * (N / BN) * (EPI == EPI_PARTIAL ? ep.split_k : 1);
     size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
     const size_t stage_out = (size_t)BM * (BN * (EPI == EPI_PARTIAL ? 4 : 2) + 16);  // LDS-staged epilogue
@@ -580,6 +587,19 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
 }
 
 extern "C" void dlms_gemm_force_tile(int id) { g_force_tile = id; }
+// launches issued so far with a BM x BN tile (BM in 32/64/128/256, BN in 64/96/128/256); reset: -1, -1
+extern "C" long dlms_gemm_tile_count(int bm, int bn) {
+    const int BMS[4] = {32, 64, 128, 256}, BNS[4] = {64, 96, 128, 256};
+    if (bm < 0) {
+        for (auto& row : g_tile_count)
+            for (auto& c : row) c.store(0);
+        return 0;
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            if (BMS[i] == bm && BNS[j] == bn) return g_tile_count[i][j].load();
+    return -1;
+}
 
 extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                 const GemmEpi* ep, hipStream_t stream) {

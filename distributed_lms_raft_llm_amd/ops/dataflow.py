@@ -39,7 +39,7 @@ class DfLayer(ctypes.Structure):
 
 
 _INT_FIELDS = ("R", "D", "H", "L", "V", "T", "seen_words", "eos", "nsteps", "A", "C", "max_nq", "swl", "ring_bytes",
-               "ldx", "n_slots", "P", "nt_weights", "ko", "kf")
+               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop")
 
 
 class DfArgs(ctypes.Structure):
@@ -55,7 +55,13 @@ LDS_MAX = 160 * 1024
 SUPPORTED_D = (128, 256, 768, 1024)  # larger d: the per-CU MLP region outgrows the ring (round 4)
 MAX_ROWS = 2
 ERRORS = {1: "arrival-counter wait timed out", 2: "q/k/v granule wait timed out", 3: "LDS hand-off wait timed out",
-          4: "weight loader timed out"}
+          4: "weight loader timed out", 5: "injected fault (test hook)"}
+NOT_RESIDENT = -2  # dataflow.hip DF_NOT_RESIDENT: the device cannot hold the whole grid at once
+
+
+class DataflowUnavailable(RuntimeError):
+    """The launch was refused before anything ran (the grid cannot be co-resident): serve the
+    launch-per-op path instead."""
 
 
 def _bind_once():
@@ -240,13 +246,33 @@ class DataflowDecoder:
                             lw.ln2_g.data_ptr(), lw.ln2_b.data_ptr(), lw.b_fc.data_ptr(), lw.b_p.data_ptr(),
                             eng.kv[l, 0].data_ptr(), eng.kv[l, 1].data_ptr())
         self.layer_tab = torch.frombuffer(bytearray(bytes(lt)), dtype=torch.uint8).to(dev)
+        # err[0..3]: code, block, step, site of the first abort; err[4]: 1 + steps run once CU 0
+        # committed the row state (0: the launch changed no row state -- nothing to undo)
         self.err = torch.zeros(16, dtype=torch.int32, device=dev)
         self._scratch: dict[int, torch.Tensor] = {}
         self.slots = torch.arange(MAX_ROWS, dtype=torch.int32, device=dev)
+        # per-launch constants (the continuous batcher launches once per decode chunk)
+        self._ring_bytes = {R: self._ring_bytes_for(R) for R in range(1, MAX_ROWS + 1)}
+        self._window = ring_window(self.cus, cfg.n_embd, self.ko, self.kf, self.NC)
+        self._exp_mlp = [sum(1 for i in range(G) if i % self.COPIES == c) for c in range(self.COPIES)]
+        self._exp_att = [sum(1 for i, cu in enumerate(self.cus) if cu.nk and i % self.COPIES == c)
+                         for c in range(self.COPIES)]
+        # cooperative launch (the runtime guarantees the grid is co-resident); DLMS_DF_COOP=0: plain
+        self.coop = os.environ.get("DLMS_DF_COOP", "1") != "0"
+        self._fault_step = -1
+        self.launches = 0
 
-    def ring_bytes(self, R: int) -> int:
+    def _ring_bytes_for(self, R: int) -> int:
         fixed = self.L.dlms_df_lds_fixed(self.eng.cfg.n_embd, R, self.max_nq, self.swl)
         return (LDS_MAX - fixed) // 8192 * 8192  # a multiple of the loader's 8 KiB batches
+
+    def ring_bytes(self, R: int) -> int:
+        return self._ring_bytes[R]
+
+    def inject_fault(self, step: int = 0):
+        """Test hook: the NEXT launch aborts at decode step ``step`` of the launch exactly as a
+        timed-out hand-off would (the last CU raises the error word, everyone drains)."""
+        self._fault_step = int(step)
 
     NC = 4          # compute waves per CU (dataflow.hip NC)
     BATCH = 8192    # loader batch bytes (dataflow.hip BATCH)
@@ -258,10 +284,10 @@ class DataflowDecoder:
         round-robin to the NC waves, NC groups.  The loader only fetches whole 8 KiB batches that
         fit behind that prefix, so a launch needs ``ring_window() + BATCH <= ring_bytes`` or a wave
         would wait forever for bytes the loader may not fetch (caught as a hand-off timeout)."""
-        return ring_window(self.cus, self.eng.cfg.n_embd, self.ko, self.kf, self.NC)
+        return self._window
 
     def fits(self, R: int) -> bool:
-        return self.ring_window() + self.BATCH <= self.ring_bytes(R)
+        return self._window + self.BATCH <= self._ring_bytes[R]
 
     def step_words(self, R: int) -> int:
         return int(self.L.dlms_df_step_words(R, self.eng.cfg.n_embd, self.eng.cfg.n_layer, self.COPIES))
@@ -317,13 +343,32 @@ class DataflowDecoder:
         a.eps, a.penalty = cfg.layer_norm_epsilon, float(penalty)
         a.nt_weights = int(os.environ.get("DLMS_DF_NT", "0") == "1")
         a.ko, a.kf = self.ko, self.kf
+        a.fault_step, self._fault_step = self._fault_step, -1
+        a.coop = int(self.coop)
         for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
-            a.exp_mlp[c] = sum(1 for i in range(self.G) if i % self.COPIES == c)
-            a.exp_att[c] = sum(1 for i, cu in enumerate(self.cus) if cu.nk and i % self.COPIES == c)
-        _check(self.L.dlms_dataflow_decode(ctypes.byref(a), self.G, _stream()), "dlms_dataflow_decode")
+            a.exp_mlp[c] = self._exp_mlp[c]
+            a.exp_att[c] = self._exp_att[c]
+        rc = self.L.dlms_dataflow_decode(ctypes.byref(a), self.G, _stream())
+        if rc == NOT_RESIDENT:
+            raise DataflowUnavailable(f"dataflow decode: a grid of {self.G} workgroups cannot be co-resident")
+        _check(rc, "dlms_dataflow_decode")
+        self.launches += 1
+
+    def status_async(self):
+        """The last launch's error words as a copy in flight (``HostResult``; ``.result()`` ->
+        (code, block, step, site, committed steps))."""
+        from ..engine.gpt2_engine import HostResult
+
+        h = torch.empty(5, dtype=torch.int32, pin_memory=True)
+        h.copy_(self.err[:5], non_blocking=True)
+        return HostResult(lambda: tuple(h.tolist()), keep=(h,))
+
+    @staticmethod
+    def describe(st) -> str:
+        return f"dataflow decode: {ERRORS.get(st[0], st[0])} (block {st[1]}, step {st[2]}, site {st[3]})"
 
     def check(self):
         """Raise if the last launch gave up on a hand-off (synchronises)."""
-        e = self.err[:4].cpu().tolist()
-        if e[0]:
-            raise RuntimeError(f"dataflow decode: {ERRORS.get(e[0], e[0])} (block {e[1]}, step {e[2]}, site {e[3]})")
+        st = tuple(self.err[:5].cpu().tolist())
+        if st[0]:
+            raise RuntimeError(self.describe(st))

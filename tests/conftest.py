@@ -7,12 +7,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# The engine serves GPT-2-124M batch-1 decode with the persistent dataflow kernel by default; the
-# engine / serving tests pin the launch-per-op latency path they were written for (several compare
-# engines token for token, and the two paths sum in different orders).  tests/test_dataflow_gpu.py
-# turns the dataflow path on explicitly and checks it against the fp32 oracle and that path, and
-# __graft_entry__.smoke() runs it at batch 1.
-os.environ.setdefault("DLMS_DATAFLOW", "0")
+# The engine's shipped defaults run in every test (batch-1 GPT-2-124M / medium decode on the
+# persistent dataflow kernel included); the few tests written for a specific launch-per-op path
+# and comparing it token for token pin DLMS_DATAFLOW=0 themselves.
 
 
 def pytest_configure(config):

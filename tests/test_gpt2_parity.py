@@ -60,3 +60,24 @@ def test_model_sizes_match_published_configs(name, hf_name):
     assert (cfg.vocab_size, cfg.n_positions, cfg.eos_token_id, cfg.layer_norm_epsilon) == \
         (d.vocab_size, d.n_positions, d.eos_token_id, d.layer_norm_epsilon)
     assert cfg.n_inner == 4 * cfg.n_embd and cfg.head_dim == 64
+
+
+def test_batched_teacher_forced_oracle_equals_per_row():
+    """The batched margin oracle (used for the 1024-row production-path test) gives the per-row
+    oracle's results, including the mismatches of a corrupted sequence."""
+    from distributed_lms_raft_llm_amd.models.gpt2 import (reference_generate, teacher_forced_check,
+                                                           teacher_forced_check_batch)
+
+    cfg = gpt2_config("gpt2-tiny")
+    m = GPT2Reference(cfg, init_gpt2_weights(cfg, seed=0))
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(0, cfg.vocab_size - 1, (n,), generator=g).tolist() for n in (3, 9, 5, 29)]
+    seqs = reference_generate(m, prompts, max_length=30)
+    seqs[1][12] = (seqs[1][12] + 1) % cfg.vocab_size
+    a = [teacher_forced_check(m, s, len(p)) for s, p in zip(seqs, prompts)]
+    b = teacher_forced_check_batch(m, seqs, [len(p) for p in prompts], chunk=3)
+    assert a[1]["mismatches"] and not a[0]["mismatches"]
+    for x, y in zip(a, b):
+        assert (x["positions"], x["decisive"]) == (y["positions"], y["decisive"])
+        assert [t[:3] for t in x["mismatches"]] == [t[:3] for t in y["mismatches"]]
+        assert abs(x["min_margin"] - y["min_margin"]) < 1e-4

@@ -455,3 +455,61 @@ def test_gemm_gelu_with_folded_layernorm(M, N, K):
     # and against the unfused path the engine used before (bf16 LN output -> GELU GEMM)
     unfused = ops.gemm(ln.to(torch.bfloat16), w, ops.EPI_GELU_TANH, bias=b)
     assert (out.float() - unfused.float()).abs().max().item() < 0.1
+
+
+@pytest.mark.parametrize("M", [257, 384, 512])
+@pytest.mark.parametrize("epi", ["qkv", "gelu_tanh", "partial_ln"])
+def test_gemm96_headline_instantiations(M, epi):
+    """The exact 64x96 instantiations every BENCH decode step launches on its 512-row halves
+    (gemm.hip: 256 < M <= 512): QKV N 2304 / K 768 with the K/V scatter into a [slots][H][T][64]
+    cache, c_fc + GELU-tanh N 3072 / K 768, and c_proj EPI_PARTIAL N 768 / K 3072 split 4 followed
+    by the add + LayerNorm that sums its slabs -- each vs fp32, and each asserted to dispatch the
+    64x96 tile (VERDICT r3 next #4)."""
+    ops = _ops()
+    D = 768
+    ops.gemm_tile_reset()
+    if epi == "qkv":
+        H, S, T = 12, 4, 150
+        a, w = _bf(M, D, seed=41), _bf(3 * D, D, scale=0.05, seed=42)
+        bias = torch.randn(3 * D, device=DEV) * 0.1
+        q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+        kc = torch.zeros(S * (M // S + 1), H, T, 64, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros_like(kc)
+        # decode-shaped rows: every row its own slot at its own position
+        slot = torch.randperm(kc.shape[0], generator=torch.Generator().manual_seed(M))[:M].to(torch.int32).to(DEV)
+        pos = (torch.arange(M, device=DEV) * 37 % T).to(torch.int32)
+        ops.gemm(a, w, ops.EPI_QKV, bias=bias, q_out=q, k_cache=kc, v_cache=vc, row_slot=slot, row_pos=pos)
+        assert ops.gemm_tile_count(64, 96) == 1
+        ref = a.float() @ w.float().t() + bias
+        torch.testing.assert_close(q.float(), ref[:, :D], atol=2e-2, rtol=2e-2)
+        sl, ps = slot.long(), pos.long()
+        k_rows = kc[sl, :, ps].reshape(M, D).float()
+        v_rows = vc[sl, :, ps].reshape(M, D).float()
+        torch.testing.assert_close(k_rows, ref[:, D:2 * D], atol=2e-2, rtol=2e-2)
+        torch.testing.assert_close(v_rows, ref[:, 2 * D:], atol=2e-2, rtol=2e-2)
+        assert int((kc != 0).sum()) == M * D  # nothing written outside the rows' (slot, pos)
+    elif epi == "gelu_tanh":
+        N = 4 * D
+        a, w = _bf(M, D, seed=43), _bf(N, D, scale=0.05, seed=44)
+        bias = torch.randn(N, device=DEV) * 0.1
+        out = ops.gemm(a, w, ops.EPI_GELU_TANH, bias=bias)
+        assert ops.gemm_tile_count(64, 96) == 1
+        ref = torch.nn.functional.gelu(a.float() @ w.float().t() + bias, approximate="tanh")
+        torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    else:
+        K = 4 * D
+        a, w = _bf(M, K, seed=45), _bf(D, K, scale=0.02, seed=46)
+        parts = torch.full((4, M, D), float("nan"), device=DEV)  # every slab element must be written
+        ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=4)
+        assert ops.gemm_tile_count(64, 96) == 1
+        ref_parts = torch.stack([a[:, s * D:(s + 1) * D].float() @ w[:, s * D:(s + 1) * D].float().t()
+                                 for s in range(4)])
+        torch.testing.assert_close(parts, ref_parts, atol=1e-2, rtol=1e-3)
+        bias = torch.randn(D, device=DEV) * 0.1
+        g, b = 1 + 0.1 * torch.randn(D, device=DEV), 0.1 * torch.randn(D, device=DEV)
+        x = torch.randn(M, D, device=DEV)
+        xr = x + ref_parts.sum(0) + bias
+        out = ops.add_layernorm(x, g, b, 1e-5, parts=parts, nsplit=4, bias=bias)
+        torch.testing.assert_close(x, xr, atol=1e-2, rtol=1e-3)  # residual updated in place
+        ref = torch.nn.functional.layer_norm(xr, (D,), g, b, 1e-5)
+        torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)

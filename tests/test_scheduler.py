@@ -16,12 +16,12 @@ def next_token(seq):
     return (sum(seq) * 31 + len(seq) * 7) % V
 
 
-def solo(prompt, T):
+def solo(prompt, T, stop_at_eos=True):
     seq = list(prompt)
     while len(seq) < T:
         t = next_token(seq)
         seq.append(t)
-        if t == EOS:
+        if t == EOS and stop_at_eos:
             break
     return seq
 
@@ -241,3 +241,86 @@ def test_stalled_tp_peer_fails_requests_instead_of_returning_garbage():
     with pytest.raises(RuntimeError):
         cb.submit([4])
     cb.stop()
+
+
+def test_cancelled_caller_does_not_kill_the_batcher():
+    """the aio servicer awaits ``asyncio.wrap_future(batcher.submit(...))`` under
+    ``wait_for``; a timeout or client cancel cancels that chain.  A request cancelled while it runs
+    must not make ``_retire``'s ``set_result`` raise (which used to fail the batcher and exit the
+    replica): its slot is freed and every other request is served."""
+    import asyncio
+
+    eng = FakeSlotEngine(max_batch=2, max_length=60)
+    eng.stop_at_eos = False
+    cb = ContinuousBatcher(eng, chunk=1)
+
+    async def ask(prompt, timeout):
+        return await asyncio.wait_for(asyncio.wrap_future(cb.submit(prompt)), timeout)
+
+    async def main():
+        res = await asyncio.gather(ask([1, 2], 0.005), ask([3], 0.005), ask([4, 5], 30.0), ask([6], 30.0),
+                                   return_exceptions=True)
+        return res
+
+    try:
+        res = asyncio.run(main())
+        assert isinstance(res[0], asyncio.TimeoutError) and isinstance(res[1], asyncio.TimeoutError)
+        assert res[2] == solo([4, 5], 60, False) and res[3] == solo([6], 60, False)
+        time.sleep(0.1)  # the abandoned requests run to the end and retire
+        assert cb.failed is None
+        assert cb.submit([7]).result(10) == solo([7], 60, False)
+    finally:
+        cb.stop()
+    assert cb.failed is None
+
+
+def test_cancelled_while_queued_is_never_admitted():
+    eng = FakeSlotEngine(max_batch=1, max_length=30)
+    eng.stop_at_eos = False
+    cb = ContinuousBatcher(eng, chunk=1)
+    try:
+        f1 = cb.submit([1])
+        f2 = cb.submit([2])  # queued behind f1 (one slot)
+        assert f2.cancel()
+        assert f1.result(10) == solo([1], 30, False)
+        assert cb.submit([3]).result(10) == solo([3], 30, False)
+    finally:
+        cb.stop()
+    assert cb.completed == 2 and cb.failed is None
+
+
+def test_dataflow_abort_makes_no_progress_and_is_retried():
+    """A chunk whose persistent dataflow launch aborted commits no row state (ops/csrc/dataflow.hip):
+    the batcher counts it, gives the live requests their step budget back, and the outputs are
+    exactly those of an engine that never aborted."""
+    from distributed_lms_raft_llm_amd.utils.metrics import METRICS
+
+    class AbortingEngine(AsyncFakeEngine):
+        def __init__(self):
+            super().__init__(max_batch=2, max_length=40)
+            self.stop_at_eos = False
+            self.chunks = 0
+            self._aborted = False
+
+        def decode(self, B, steps, penalty):
+            self.chunks += 1
+            self._aborted = self.chunks in (2, 3, 7)
+            if self._aborted:  # the launch drained without committing: nothing advanced
+                self.buckets.append(B)
+                return
+            super().decode(B, steps, penalty)
+
+        def dataflow_status_async(self):
+            a = self._aborted
+            return SimpleNamespace(result=lambda: a)
+
+    before = METRICS.snapshot()["counters"].get("tutor_dataflow_aborts", 0)
+    eng = AbortingEngine()
+    cb = ContinuousBatcher(eng, chunk=4)
+    try:
+        prompts = [[1, 2, 3], [9], [4, 4]]
+        outs = [f.result(10) for f in [cb.submit(p) for p in prompts]]
+    finally:
+        cb.stop()
+    assert outs == [solo(p, 40, False) for p in prompts]
+    assert METRICS.snapshot()["counters"]["tutor_dataflow_aborts"] - before == 3
