@@ -331,6 +331,23 @@ class HipGPT2Engine:
             for lw in self.w.layers:
                 if lw.w_p_sl is None:
                     lw.w_p_sl = ops.slice_cproj(lw.w_p)
+        # TP > 1, the latency path (<= tp_fused_rows rows): every rank runs a layer as six kernels --
+        # [LN1 + QKV of its heads] -> attention -> [out-projection partial] -> xGMI all-reduce ->
+        # [+ attention + b_o, LN2, c_fc shard, GELU, c_proj slice into an int64 fixed-point
+        # accumulator; rank 0 also adds the residual + b_p] -> integer xGMI all-reduce, which IS the
+        # next residual on every rank (exact, order-independent) -- against eight launch-per-op
+        # kernels (separate c_fc and c_proj, two split partial slabs to sum).  DLMS_TP_FUSED=0: off.
+        self.tp_fused = (self.tp_size > 1 and self.small_max > 0 and not self.w.fp8 and
+                         cfg.n_embd in ops.SKINNY_MLP_WIDTHS and self.w.ffn_local % 16 == 0 and
+                         os.environ.get("DLMS_TP_FUSED", "1") != "0")
+        self.tp_fused_steps = 0
+        self.tp_fused_rows = min(self.small_max, int(os.environ.get("DLMS_TP_FUSED_ROWS", "4"))) if self.tp_fused else 0
+        if self.tp_fused:
+            for lw in self.w.layers:
+                if lw.w_o_sh is None:
+                    lw.w_o_sh = ops.shuffle_weight(lw.w_o)
+                if lw.w_p_sl is None:
+                    lw.w_p_sl = ops.slice_cproj(lw.w_p)
         # LM head of the throughput path (>= PS_LM_MIN_ROWS rows): panel-resident gemm_ps on a
         # pre-shuffled copy of the (tied) LM-head shard: 67 vs 87 us at 512 rows, 114 vs 146 at 1024
         # (profiles/r2_gemm_ps_vs_tiled.log)
@@ -388,8 +405,9 @@ class HipGPT2Engine:
         # second residual buffer: the latency path's fused add+LN kernels advance x by ping-pong
         self.x2 = torch.zeros(min(B, 64), D, dtype=f32, device=dev)
         # the fused MLP's ping-pong int64 fixed-point residual (batch 1)
-        self.xr = (torch.zeros(2, ops.fix_copies(), max(1, min(self.fused_mlp_rows, B)), D, dtype=torch.int64, device=dev)
-                   if self.fused_mlp else None)
+        xr_rows = max(self.fused_mlp_rows, self.tp_fused_rows)
+        self.xr = (torch.zeros(2, ops.fix_copies(), max(1, min(xr_rows, B)), D, dtype=torch.int64, device=dev)
+                   if (self.fused_mlp or self.tp_fused) else None)
         # cross-workgroup split attention (few rows, long caches): partials + arrival counters
         self.attn_ws = ops.AttnSplitWorkspace(self.SPLIT_ATTN_MAX_PAIRS, 2, dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
@@ -429,6 +447,15 @@ class HipGPT2Engine:
                 self.xgmi.all_reduce_(t)
             else:
                 dist.all_reduce(t, group=self.tp_group)
+
+    def _all_reduce_i64(self, t: torch.Tensor):
+        """Integer all-reduce of a contiguous int64 tensor (the TP fused layer's fixed point)."""
+        import torch.distributed as dist
+
+        if self.xgmi is not None and self.xgmi.fits(t):
+            self.xgmi.all_reduce_i64_(t)
+        else:
+            dist.all_reduce(t, group=self.tp_group)
 
     def _gather_keys(self, B: int, P: int) -> torch.Tensor:
         """Argmax keys as a [B, P] view: the LM head's per-tile partials (TP=1), or one reduced key
@@ -856,6 +883,11 @@ class HipGPT2Engine:
             ops.ln_fix(self.xr[(len(self.w.layers) - 1) % 2, :, :B], self.w.lnf_g, self.w.lnf_b, eps, self.h[:B])
             self._lm_head_and_update(self.h[:B], B, penalty)
             return
+        if tp and self.tp_fused and B <= self.tp_fused_rows and ops.skinny_mlp_cg(self.cfg.n_embd, B) > 0:
+            self._decode_layers_tp_fused(r, B)
+            ops.ln_fix(self.xr[(len(self.w.layers) - 1) % 2, :, :B], self.w.lnf_g, self.w.lnf_b, eps, self.h[:B])
+            self._lm_head_and_update(self.h[:B], B, penalty)
+            return
         for li, lw in enumerate(self.w.layers):
             kc, vc = self.kv[li, 0], self.kv[li, 1]
             if pend is None:
@@ -933,6 +965,27 @@ class HipGPT2Engine:
                 ops.skinny_gemm(self.att[:B], lw.w_o_sh, ops.EPI_F32, bias=lw.b_o, out=xin if li == 0 else xin[0])
                 ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc)
             xin = acc
+
+    def _decode_layers_tp_fused(self, r, B: int):
+        """TP > 1 latency path, six kernels per layer on every rank (see ``tp_fused`` in __init__):
+        the replicated residual enters as the f32 embedding rows (layer 0) or the all-reduced
+        fixed-point accumulator of the previous layer; the final residual is xr[(L - 1) % 2]."""
+        eps = self.cfg.layer_norm_epsilon
+        xin = self.x[:B]
+        base = self.tp_rank == 0
+        self.tp_fused_steps += 1  # (host-side count of steps issued on this path: tests assert it)
+        for li, lw in enumerate(self.w.layers):
+            kc, vc = self.kv[li, 0], self.kv[li, 1]
+            acc_all = self.xr[li % 2]  # [copies, rows, d], contiguous: the integer all-reduce's message
+            ops.skinny_addln_gemm(xin, lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, bias=lw.b_qkv, q_out=r.q,
+                                  k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos, zero=acc_all)
+            self._attn(r, li)
+            ops.skinny_gemm(self.att[:B], lw.w_o_sh, ops.EPI_PARTIAL, out=self.parts[0, :B])
+            self._all_reduce(self.parts[0, :B])
+            ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc_all[:, :B],
+                           parts=self.parts[:1, :B], nsplit=1, res_bias=lw.b_o, base=base)
+            self._all_reduce_i64(acc_all)
+            xin = acc_all[:, :B]
 
     def _small_overlap_ok(self, B: int) -> bool:
         k = self.small_overlap_parts
@@ -1107,7 +1160,9 @@ class HipGPT2Engine:
     PREFILL_GRAPH_CACHE = 32
 
     def _prefill_graph_ok(self, R: int, n: int) -> bool:
-        if not (self.use_graph and self.prefill_graphs and self.tp_size == 1 and R <= self.PREFILL_GRAPH_MAX_ROWS):
+        if not (self.use_graph and self.prefill_graphs and R <= self.PREFILL_GRAPH_MAX_ROWS):
+            return False
+        if self.tp_size > 1 and not self._tp_capturable(R):
             return False
         key = (R, n)
         if key in self._pgraphs:
@@ -1116,6 +1171,15 @@ class HipGPT2Engine:
             self._pseen.clear()
         self._pseen[key] = self._pseen.get(key, 0) + 1
         return self._pseen[key] >= 2 and len(self._pgraphs) < self.PREFILL_GRAPH_CACHE
+
+    def _tp_capturable(self, R: int) -> bool:
+        """A TP prefill of R packed rows can be captured: every collective in it is an xGMI kernel
+        (its messages fit the slab) or the group is RCCL (capturable); gloo calls are eager-only."""
+        import torch.distributed as dist
+
+        if self.xgmi is None:
+            return False
+        return R * self.cfg.n_embd * 4 <= self.xgmi.slab_bytes or dist.get_backend(self.tp_group) == "nccl"
 
     def _prefill_graphed(self, tok, pos, slot, last, slots, lens, penalty: float):
         R, n = tok.size, slots.size

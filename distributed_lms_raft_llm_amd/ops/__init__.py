@@ -159,7 +159,7 @@ def _bind(L):
                                    ctypes.POINTER(GemmEpi), I, ctypes.c_longlong, P, I, P],
         "dlms_skinny_mlp_cg": [I, I, I],
         "dlms_skinny_mlp": [P, I, I, ctypes.c_longlong, P, I, ctypes.c_longlong, I, P, P, P, F, P, P, P, P, P, I,
-                            ctypes.c_longlong, I, I, I, I, P],
+                            ctypes.c_longlong, I, I, I, I, I, P],
         "dlms_ln_fix": [P, I, ctypes.c_longlong, P, P, F, P, I, I, I, P],
         "dlms_fix_copies": [],
         "dlms_skinny_addln_max_rows": [I],
@@ -177,6 +177,7 @@ def _bind(L):
                        "dlms_xgmi_error": [P, I, ctypes.POINTER(ctypes.c_uint)],
                        "dlms_xgmi_error_async": [P, P, P],
                        "dlms_xgmi_allreduce_f32": [ctypes.POINTER(XgmiArgs), P],
+                       "dlms_xgmi_allreduce_i64": [ctypes.POINTER(XgmiArgs), P],
                        "dlms_xgmi_allgather_u64": [ctypes.POINTER(XgmiArgs), P]}.items():
         fn = getattr(L, name)
         fn.argtypes = args
@@ -994,11 +995,15 @@ def skinny_mlp_cg(K: int, M: int, want: int = 0) -> int:
 
 
 def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tensor, b_fc, w_p_sl: torch.Tensor, b_p,
-               r_out: torch.Tensor, *, parts=None, nsplit: int = 0, res_bias=None, cg: int = 0):
-    """Fused latency-path MLP (TP=1, M <= 8 rows, d in SKINNY_MLP_WIDTHS):
+               r_out: torch.Tensor, *, parts=None, nsplit: int = 0, res_bias=None, cg: int = 0, base: bool = True):
+    """Fused latency-path MLP (M <= 8 rows, d in SKINNY_MLP_WIDTHS):
 
         v = x_in + res_bias + sum(parts[:nsplit]);  h = bf16(gelu(bf16(LN(v)) @ W_fc.T + b_fc))
-        r_out += fix(v + h @ W_p.T + b_p)
+        r_out += fix(v + h @ W_p.T + b_p)          (base=False: r_out += fix(h @ W_p.T) only)
+
+    Tensor parallel (``W_fc`` / ``b_fc`` the rank's column shard, ``W_p`` its row-parallel slice,
+    ``parts`` the all-reduced attention partial, nsplit 1): rank 0 runs with base=True, the others
+    with base=False, and an integer all-reduce of ``r_out`` over the group is the next residual.
 
     ``x_in``: f32 [M, d] or int64 fixed point [fix_copies(), M, d]; ``r_out``: int64 fixed point
     [fix_copies(), M, d], ZERO on entry (``skinny_addln_gemm(zero=...)`` clears it), must not alias
@@ -1040,8 +1045,8 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
         _req(t, torch.float32, n, 1)
         if t.numel() != size:
             raise ValueError(f"skinny_mlp: {n} size")
-    if nsplit not in (0, 4) or (nsplit and K > 1024):
-        raise ValueError("skinny_mlp: nsplit in {0, 4} (4: d <= 1024)")
+    if nsplit not in (0, 1, 4) or (nsplit == 4 and K > 1024):
+        raise ValueError("skinny_mlp: nsplit in {0, 1, 4} (4: d <= 1024)")
     ldp, sstride = 0, 0
     if nsplit:
         _req(parts, torch.float32, "parts", 3)
@@ -1055,7 +1060,8 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
             raise ValueError("res_bias size")
     _check(lib().dlms_skinny_mlp(_p(x_in), x_in.stride(0), int(xfix), xcs, _p(parts) if nsplit else None, ldp,
                                  sstride, nsplit, _p(res_bias), _p(gamma), _p(beta), float(eps), _p(w_fc_sh), _p(b_fc),
-                                 _p(w_p_sl), _p(b_p), _p(r_out), r_out.stride(0), rcs, M, K, F, int(cg), _stream()),
+                                 _p(w_p_sl), _p(b_p), _p(r_out), r_out.stride(0), rcs, M, K, F, int(cg), int(bool(base)),
+                                 _stream()),
            "dlms_skinny_mlp")
     return r_full
 

@@ -26,15 +26,22 @@
 // Per layer (TP=1):
 //   E1  residual complete (previous MLP's atomics + counter, or the embedding) -> every CU: LN1,
 //       its rows of W_qkv (dot) -> q/k/v as tagged 8-byte granules (+ K/V cache rows)
-//   E2  per-head granules -> the attention CUs of that head: attention over the cache, then their
-//       head dims' slice of W_o -> counted fixed-point atomics into XA
-//   E3  XA complete (every word's contribution count) -> every CU: x += XA + b_o, LN2, its c_fc
-//       rows (h = bf16(gelu(.))) and their c_proj columns -> counted fixed-point atomics into XM
+//   E2  per-head granules -> the attention CUs of that head: attention over the cache, then W_o
+//       for the CU's slice of OUTPUT columns (all 64 head dims) -> counted fixed-point atomics into XA
+//   E3  XA complete (every word's contribution count) -> every CU: x += XA + b_o, LN2, the c_fc
+//       rows of its intermediate slice (h = bf16(gelu(.))), c_proj for its slice of output columns
+//       -> counted fixed-point atomics into XM
+//   (output-column slices: a CU adds d / GS or d / J residual words per row, not d -- the counted
+//   atomics' issue and memory-side time set the publish and edge costs; ops/dataflow.py assign())
 // then ln_f + this CU's LM-head rows + penalty + argmax key -> 64-bit atomicMax + counter -> every
 // CU reads the token and the next step starts.  Every CU keeps its own copy of the residual stream
 // as int64 fixed point (value * 2^32, DLMS_FIX_SCALE in skinny.hip) and adds each edge's summed
 // contributions: integer adds commute, so results do not depend on arrival order and all copies
 // agree bit for bit.
+//
+// Commit: CU 0 writes the row state back (lengths, tokens, penalty bitmap) only after every step it
+// ran has completed; an aborted launch commits nothing, so a retry -- another launch or the
+// launch-per-op path -- starts from exactly the state this launch found.
 //
 // Hand-off memory ("scratch") is FRESH per step (zeroed before the launch), so nothing a CU reads
 // was ever cached before its final value was written; payload/counter traffic is sc1 (agent scope),
@@ -62,7 +69,7 @@ constexpr int INFL = DF_INFL;         // LDS-DMA units (1 KiB) in flight per loa
 #ifndef DF_COPIES
 #define DF_COPIES 2
 #endif
-constexpr int COPIES = DF_COPIES;     // fixed-point residual copies (CU c adds into copy c % COPIES)
+constexpr int COPIES = DF_COPIES;     // fixed-point residual copies (each CU adds into its Cu::acp / mcp)
 constexpr int LDS_MAX = 160 * 1024;
 // a streamed weight row: d bf16 + 32 bytes of padding, so the 16 rows of an MFMA B fragment sit on
 // distinct 16-B LDS slots (a 1536-B row is 0 mod 256 B: 8-way ds_read_b128 conflicts unpadded)
@@ -74,12 +81,15 @@ constexpr unsigned long long TIMEOUT_TICKS = 20000000ull;  // 0.2 s of the 100 M
 typedef unsigned long long u64;
 typedef long long i64;
 
-struct Cu {           // per-CU assignment (host-built table, ops/dataflow.py mirrors it)
+struct Cu {           // per-CU assignment (host-built table, ops/dataflow.py assign() mirrors it)
     int q0, nq;       // W_qkv rows [q0, q0 + nq)
-    int f0, nf;       // (c_fc row, c_proj column) pairs [f0, f0 + nf)
+    int f0, nf;       // intermediate (c_fc row) slice [f0, f0 + nf)
     int v0, nv;       // LM-head (wte) rows [v0, v0 + nv)
-    int ah, ak0, nk;  // attention head (-1: none) and its head dims [ak0, ak0 + nk) of W_o
-    int pad0, pad1, pad2;
+    int ah;           // attention head (-1: none)
+    int ao0, aon;     // its W_o output columns [ao0, ao0 + aon) (all 64 head dims)
+    int pd0, pdn;     // c_proj output columns [pd0, pd0 + pdn) of the slice
+    int acp, mcp;     // residual copy of the attention / MLP contributions
+    int pad;
     long long off;    // byte offset of this CU's packed row stream
     long long step_bytes;
 };
@@ -405,7 +415,7 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
     const u64* keys = reinterpret_cast<const u64*>(lds + ly.keys);
     const int L = a.L, H = a.H, T = a.T, C = a.C, G = gridDim.x;
     const Scr sc = scratch_layout(R, D, L, C);
-    const int copy = blockIdx.x % COPIES, shard = blockIdx.x % SHARDS;
+    const int shard = blockIdx.x % SHARDS;
     const int D3 = 3 * D;
 
     // ---- row state
@@ -545,14 +555,13 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
                 lds_st(ctl + C_READY, pid);
                 if (!(ok = wait_phdone(ctl, pid, a, s))) break;
                 stamp(a, s, l, 6, lane);
-                u64* X = sw + (2 * l) * sc.xw;
+                u64* X = sw + (2 * l) * sc.xw + (size_t)cu.acp * R * D + cu.ao0;
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int i = 0; i < EPL; ++i) {
                         const int e = lane + 64 * i;
-                        const float p = part[r * D + e];
-                        gadd64(X + ((size_t)copy * R + r) * D + e, counted(f2fix(p)));
+                        if (e < cu.aon) gadd64(X + (size_t)r * D + e, counted(f2fix(part[r * D + cu.ao0 + e])));
                     }
                 stamp(a, s, l, 7, lane);
             }
@@ -577,14 +586,13 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
             if (!(ok = wait_phdone(ctl, pid, a, s))) break;
             stamp(a, s, l, 10, lane);
             {
-                u64* X = sw + (2 * l + 1) * sc.xw;
+                u64* X = sw + (2 * l + 1) * sc.xw + (size_t)cu.mcp * R * D + cu.pd0;
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int i = 0; i < EPL; ++i) {
                         const int e = lane + 64 * i;
-                        const float p = part[r * D + e];
-                        gadd64(X + ((size_t)copy * R + r) * D + e, counted(f2fix(p)));
+                        if (e < cu.pdn) gadd64(X + (size_t)r * D + e, counted(f2fix(part[r * D + cu.pd0 + e])));
                     }
                 stamp(a, s, l, 11, lane);
             }
@@ -853,14 +861,16 @@ __device__ __forceinline__ f32x4_t mfma_rows16(const char* ring, unsigned gro, u
     return acc0 + acc1;
 }
 
-// this wave's 16-column output tiles t = w, w + NC, ... of a K-major block [D][KP] at ring offset
-// bro: out[m][16 t + l] = sum_k A[m][k] * Blk[16 t + l][k] (v_mfma_f32_16x16x16_bf16 per 16-deep k
-// block; afr[kb]: this lane's A fragment, row l & 15, k = 16 kb + 4 (l >> 4) .. + 4).  Every B
-// fragment of the wave is read before the first MFMA; results go to part[m][..] (lanes < 16).
+// this wave's 16-row output tiles t = w, w + NC, ... (t < ntiles) of a K-major block [16 ntiles][KP]
+// at ring offset bro (bro < RB): out[m][o0 + 16 t + l] = sum_k A[m][k] * Blk[16 t + l][k]
+// (v_mfma_f32_16x16x16_bf16 per 16-deep k block; afr[kb]: this lane's A fragment, row l & 15,
+// k = 16 kb + 4 (l >> 4) .. + 4).  Every B fragment of the wave is read before the first MFMA;
+// results go to part[m][o0 + ..] (lanes < 16).  Offsets stay below 2 RB (a block is smaller than
+// the ring), so one conditional subtract wraps them -- no integer division per fragment.
 template <int D, int R, int KB>
-__device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsigned RB, int KP, int nkb,
-                                           const bf16x4_t (&afr)[KB], float* part, int w, int lane) {
-    constexpr int TPW = D / 16 / NC;  // tiles per wave
+__device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsigned RB, int KP, int nkb, int ntiles,
+                                           int o0, const bf16x4_t (&afr)[KB], float* part, int w, int lane) {
+    constexpr int TPW = D / 16 / NC;  // the most tiles a wave may own (a block of all D outputs)
     static_assert((D / 16) % NC == 0, "tiles per wave");
     const int n = lane & 15, kq = lane >> 4;
     const unsigned base = bro + (unsigned)((16 * w + n) * KP + 4 * kq) * 2u;
@@ -874,15 +884,18 @@ __device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsig
         bf16x4_t bv[TPW];
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
-            bv[j] = *reinterpret_cast<const bf16x4_t*>(ring + (base + tstep * j + 32u * kb) % RB);
+            if (w + NC * j < ntiles) bv[j] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * j + 32u * kb, RB));
 #pragma unroll
-        for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], bv[j], acc[j], 0, 0, 0);
+        for (int j = 0; j < TPW; ++j)
+            if (w + NC * j < ntiles) acc[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], bv[j], acc[j], 0, 0, 0);
     }
     if (lane < 16) {
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
+            if (w + NC * j < ntiles) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) part[r * D + 16 * (w + NC * j) + lane] = acc[j][r];
+                for (int r = 0; r < R; ++r) part[r * D + o0 + 16 * (w + NC * j) + lane] = acc[j][r];
+            }
     }
 }
 
@@ -938,7 +951,7 @@ __device__ __forceinline__ void os_merge(OnlineS& z, float m2, float l2, const f
 
 template <int D, int R, int PFG>
 __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int w, int lane) {
-    constexpr int KBMAX = 4;  // k blocks of 16 per K-major block (nf, nk <= 64)
+    constexpr int KBMAX = 4;  // k blocks of 16 per K-major block (K <= 64: a head, a slice)
     unsigned* ctl = reinterpret_cast<unsigned*>(lds + ly.ctl);
     const int* st = reinterpret_cast<const int*>(lds + ly.st);
     const bf16_t* xnb = reinterpret_cast<const bf16_t*>(lds + ly.xn);
@@ -959,10 +972,12 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
     const float penalty = a.penalty;
     const bool tracing = a.trace != nullptr;
     const Layer* layers = a.layers;
-    const int nq = cu.nq, nk = cu.nk, nf = cu.nf, nv = cu.nv, ah = cu.ah, ak0 = cu.ak0, v0 = cu.v0, f0 = cu.f0;
+    const int nq = cu.nq, nf = cu.nf, nv = cu.nv, ah = cu.ah, v0 = cu.v0, f0 = cu.f0;
+    const int ao0 = cu.ao0, aon = cu.aon, pd0 = cu.pd0, pdn = cu.pdn;
     constexpr unsigned ROWB = ROW_BYTES(D);
-    const unsigned ko_bytes = nk > 0 ? (unsigned)(D * KO * 2) : 0u;
-    const unsigned layer_bytes = (unsigned)(nq + nf) * ROWB + ko_bytes + (unsigned)(D * KF * 2);
+    const unsigned ko_bytes = ah >= 0 ? (unsigned)(aon * KO * 2) : 0u;
+    const unsigned kf_bytes = (unsigned)(pdn * KF * 2);
+    const unsigned layer_bytes = (unsigned)(nq + nf) * ROWB + ko_bytes + kf_bytes;
     const unsigned SB = (unsigned)cu.step_bytes;
     const int ts = lane >> 3, ck = lane & 7;
     const int n16 = lane & 15;
@@ -989,9 +1004,9 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
         for (int l = 0; l < L; ++l) {
             const Layer lw = layers[l];
             const unsigned lbase = sbase + (unsigned)l * layer_bytes;
-            const unsigned obase = lbase + (unsigned)nq * ROWB;          // W_o block [D][KO]
+            const unsigned obase = lbase + (unsigned)nq * ROWB;          // W_o block [aon][KO]
             const unsigned fbase = obase + ko_bytes;                     // c_fc rows
-            const unsigned pbase = fbase + (unsigned)nf * ROWB;          // c_proj block [D][KF]
+            const unsigned pbase = fbase + (unsigned)nf * ROWB;          // c_proj block [pdn][KF]
             u64 ringwait = 0;
             // ---- attention CU: prefetch this layer's cached K/V of the head (independent of q)
             uint4 kpf[R][PFG], vpf[R][PFG];
@@ -1139,15 +1154,15 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
                         lsum += mb[65] * e;
                         osum += mb[lane] * e;
                     }
-                    hb[r * 64 + lane] = f32_to_bf16(osum / lsum);  // this CU's dims: k = d - ak0
+                    hb[r * 64 + lane] = f32_to_bf16(osum / lsum);  // head dim lane: the A operand of W_o
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 bf16x4_t afr[KBMAX];
                 const int nkb = KO / 16;
-                load_afr<KBMAX, R>(hb, ak0, nk, nkb, afr, lane);
+                load_afr<KBMAX, R>(hb, 0, 64, nkb, afr, lane);  // all 64 head dims
                 if (!wait_loaded_t(ctl, fbase, a, s, &ringwait, tracing)) return;  // the whole W_o block
                 asm volatile("" ::: "memory");
-                mfma_block<D, R, KBMAX>(ring, obase % RB, RB, KO, nkb, afr, part, w, lane);
+                mfma_block<D, R, KBMAX>(ring, obase % RB, RB, KO, nkb, aon / 16, ao0, afr, part, w, lane);
                 if (w == 0) stamp(a, s, l, 21, lane);
                 lds_st(ctl + C_CONS + w, fbase >> 4);
                 lds_st(ctl + C_PHDONE + w, pid);
@@ -1173,6 +1188,9 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
                         for (int r = 0; r < R; ++r) fcp[(w * R + r) * 64 + 16 * g + lane] = acc[r];
                     }
                 }
+                // (done with the c_fc rows: the loader may overwrite them with the c_proj block, so
+                // the ring needs room for the larger of the two, not both -- GPT-2-large / XL)
+                lds_st(ctl + C_CONS + w, pbase >> 4);
                 lds_st(ctl + C_MID + w, pid);
 #pragma unroll
                 for (int w2 = 0; w2 < NC; ++w2)
@@ -1192,12 +1210,12 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
                 bf16x4_t afr[KBMAX];
                 const int nkb = KF / 16;
                 load_afr<KBMAX, R>(hb, 0, nf, nkb, afr, lane);
-                if (!wait_loaded_t(ctl, pbase + (unsigned)(D * KF * 2), a, s, &ringwait, tracing)) return;
+                if (!wait_loaded_t(ctl, pbase + kf_bytes, a, s, &ringwait, tracing)) return;
                 asm volatile("" ::: "memory");
-                mfma_block<D, R, KBMAX>(ring, pbase % RB, RB, KF, nkb, afr, part, w, lane);
+                mfma_block<D, R, KBMAX>(ring, pbase % RB, RB, KF, nkb, pdn / 16, pd0, afr, part, w, lane);
                 if (w == 0) stamp(a, s, l, 23, lane);
                 if (w == 0 && lane == 0) stamp_val(a, s, l, 12, ringwait);
-                lds_st(ctl + C_CONS + w, (pbase + (unsigned)(D * KF * 2)) >> 4);
+                lds_st(ctl + C_CONS + w, (pbase + kf_bytes) >> 4);
                 lds_st(ctl + C_PHDONE + w, pid);
             }
         }
@@ -1214,6 +1232,11 @@ __device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& 
             for (int g = w; 16 * g < nv; g += NC) {
                 const int rows = min(16, nv - 16 * g);
                 const unsigned end = vbase + (unsigned)(16 * g + rows) * ROWB;
+                // everything before this group is done with (this wave's earlier groups, and the
+                // other waves' groups are theirs): releasing it before the wait lets the loader run
+                // ahead by the whole ring, so a window of ONE 16-row group suffices (XL: 4 groups of
+                // 3.2 KB rows would not fit)
+                lds_st(ctl + C_CONS + w, (vbase + (unsigned)(16 * g) * ROWB) >> 4);
                 if (!wait_loaded_t(ctl, end, a, s, &ringwait, tracing)) return;
                 asm volatile("" ::: "memory");
                 const f32x4_t acc = mfma_rows16<D, R, NCK>(ring, (vbase + (unsigned)(16 * g) * ROWB) % RB, RB, xnb, 0, lane);

@@ -737,7 +737,8 @@ __global__ __launch_bounds__(256) void skinny_mlp_kernel(
     const void* __restrict__ x_in, int ldx, const float* __restrict__ parts, int ldp, long long split_stride,
     const float* __restrict__ res_bias, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     const bf16_t* __restrict__ Wfc_sh, const float* __restrict__ b_fc, const bf16_t* __restrict__ Wp_sl,
-    const float* __restrict__ b_p, unsigned long long* __restrict__ r_out, int ldr, long long rcs, long long xcs, int M) {
+    const float* __restrict__ b_p, unsigned long long* __restrict__ r_out, int ldr, long long rcs, long long xcs, int M,
+    int base) {
     constexpr int NW = 4;
     constexpr int K = NKB * 32;
     constexpr int WPG = NW / CG;                // waves per column group: they split its K
@@ -787,7 +788,7 @@ __global__ __launch_bounds__(256) void skinny_mlp_kernel(
 #pragma unroll
     for (int i = 0; i < NCP; ++i) {
         const int n = tid + 256 * i;
-        bp[i] = (blockIdx.x == 0 && n < K) ? b_p[n] : 0.f;
+        bp[i] = (blockIdx.x == 0 && base && n < K) ? b_p[n] : 0.f;
     }
 
     // (1) residual rows -> LN2 -> LDS image (block 0 also keeps v); (2) c_fc slice on MFMA
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(256) void skinny_mlp_kernel(
         for (int m = 0; m < ROWS; ++m) {
             if (m >= M) break;
             float v = o[m];
-            if (blockIdx.x == 0) v += v_lds[m * K + n] + bp[i];  // the residual and the c_proj bias, once
+            if (blockIdx.x == 0 && base) v += v_lds[m * K + n] + bp[i];  // the residual and the c_proj bias, once
             atomicAdd(rc + (size_t)m * ldr + n, f32_to_fix(v));
         }
     }
@@ -857,7 +858,7 @@ template <int NSPLIT, int NV4, int RPW, int NKB, int CG, bool XFIX>
 static hipError_t launch_mlp(const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
                              const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
                              const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* r_out, int ldr,
-                             long long rcs, long long xcs, int M, int F, hipStream_t stream) {
+                             long long rcs, long long xcs, int M, int F, int base, hipStream_t stream) {
     if constexpr (!mlp_fits(RPW, NKB, CG)) {
         return hipErrorInvalidValue;
     } else {
@@ -871,7 +872,7 @@ static hipError_t launch_mlp(const void* x_in, int ldx, const float* parts, int 
             attr_set = true;
         }
         hipLaunchKernelGGL((skinny_mlp_kernel<NSPLIT, NV4, RPW, NKB, CG, XFIX>), dim3(F / (16 * CG)), dim3(256), lds, stream,
-                           x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, r_out, ldr, rcs, xcs, M);
+                           x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, r_out, ldr, rcs, xcs, M, base);
         return hipGetLastError();
     }
 }
@@ -909,10 +910,10 @@ template <int NSPLIT, int NV4, int NKB, bool XFIX, int RPW>
 static hipError_t mlp_cg(int cg, const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
                          const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
                          const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* R, int ldr,
-                         long long rcs, long long xcs, int M, int F, hipStream_t stream) {
+                         long long rcs, long long xcs, int M, int F, int base, hipStream_t stream) {
 #define MLP_GO(CG_) \
     return launch_mlp<NSPLIT, NV4, RPW, NKB, CG_, XFIX>(x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, \
-                                                       b_p, R, ldr, rcs, xcs, M, F, stream)
+                                                       b_p, R, ldr, rcs, xcs, M, F, base, stream)
     switch (cg) {
         case 1: MLP_GO(1);
         case 2: MLP_GO(2);
@@ -926,8 +927,8 @@ template <int NSPLIT, int NV4, int NKB>
 static hipError_t mlp_rows(int cg, int xfix, const void* x_in, int ldx, const float* parts, int ldp, long long sstride,
                            const float* rbias, const float* g, const float* b, float eps, const bf16_t* Wfc,
                            const float* b_fc, const bf16_t* Wp, const float* b_p, unsigned long long* R, int ldr,
-                           long long rcs, long long xcs, int M, int F, hipStream_t stream) {
-#define MLP_ARGS cg, x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, R, ldr, rcs, xcs, M, F, stream
+                           long long rcs, long long xcs, int M, int F, int base, hipStream_t stream) {
+#define MLP_ARGS cg, x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, R, ldr, rcs, xcs, M, F, base, stream
     if (M <= 4) {
         if (xfix) return mlp_cg<NSPLIT, NV4, NKB, true, 1>(MLP_ARGS);
         return mlp_cg<NSPLIT, NV4, NKB, false, 1>(MLP_ARGS);
@@ -945,9 +946,9 @@ extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long 
                                       long long split_stride, int nsplit, const float* res_bias, const float* gamma,
                                       const float* beta, float eps, const void* Wfc_sh, const float* b_fc,
                                       const void* Wp_sl, const float* b_p, void* r_out, int ldr, long long rcs, int M,
-                                      int K, int F, int want_cg, hipStream_t stream) {
+                                      int K, int F, int want_cg, int base, hipStream_t stream) {
     if (M <= 0 || M > 8 || F % 16 || F <= 0) return hipErrorInvalidValue;
-    if (nsplit != 0 && (nsplit != 4 || K > 1024)) return hipErrorInvalidValue;
+    if (nsplit != 0 && nsplit != 1 && (nsplit != 4 || K > 1024)) return hipErrorInvalidValue;
     const int cg = dlms_skinny_mlp_cg(K, M, want_cg);
     if (cg == 0) return hipErrorInvalidValue;
     const bf16_t* Wf = reinterpret_cast<const bf16_t*>(Wfc_sh);
@@ -955,16 +956,24 @@ extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long 
     unsigned long long* R = reinterpret_cast<unsigned long long*>(r_out);
 #define MLP_K(NS, NV, NKB_) \
     return mlp_rows<NS, NV, NKB_>(cg, xfix, x_in, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, Wf, b_fc, Wp, \
-                                  b_p, R, ldr, rcs, xcs, M, F, stream)
+                                  b_p, R, ldr, rcs, xcs, M, F, base, stream)
+    // nsplit 1: the TP all-reduced attention partial (tensor-parallel fused layer, base = 0 on the
+    // ranks other than 0: they add only their c_proj partial, rank 0 also the residual + b_p)
     switch (K) {
         case 768:
             if (nsplit == 4) MLP_K(4, 3, 24);
+            if (nsplit == 1) MLP_K(1, 3, 24);
             MLP_K(0, 3, 24);
         case 1024:
             if (nsplit == 4) MLP_K(4, 4, 32);
+            if (nsplit == 1) MLP_K(1, 4, 32);
             MLP_K(0, 4, 32);
-        case 1280: MLP_K(0, 5, 40);
-        case 1600: MLP_K(0, 7, 50);
+        case 1280:
+            if (nsplit == 1) MLP_K(1, 5, 40);
+            MLP_K(0, 5, 40);
+        case 1600:
+            if (nsplit == 1) MLP_K(1, 7, 50);
+            MLP_K(0, 7, 50);
         default: return hipErrorInvalidValue;
     }
 #undef MLP_K

@@ -138,6 +138,38 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_f32_kernel(XgmiAr
     xgmi_finish(a, e);
 }
 
+// Integer all-reduce of int64 words (the TP fused decode's fixed-point residual partials,
+// value * 2^32): integer adds are exact and order-independent, so every rank holds the identical
+// residual without relying on a summation order.  n: int64 words, a multiple of 2.
+template <int W>
+__global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_i64_kernel(XgmiArgs a) {
+    const unsigned e = xgmi_epoch(a);
+    const long long slab_off = XGMI_HEADER_BYTES + (long long)(e & 1) * a.slab_bytes;
+    long long lo, hi;
+    xgmi_chunk(a.n / 2, lo, hi);
+    const longlong2* in = reinterpret_cast<const longlong2*>(a.in);
+    longlong2* mine = reinterpret_cast<longlong2*>(a.base[a.rank] + slab_off);
+    for (long long i = lo + threadIdx.x; i < hi; i += XGMI_THREADS) mine[i] = in[i];
+    xgmi_signal_and_wait<W>(a, e);
+    const longlong2* src[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) src[p] = reinterpret_cast<const longlong2*>(a.base[p] + slab_off);
+    longlong2* out = reinterpret_cast<longlong2*>(a.out);
+    for (long long i = lo + threadIdx.x; i < hi; i += XGMI_THREADS) {
+        longlong2 v[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p) v[p] = src[p][i];
+        longlong2 s = v[0];
+#pragma unroll
+        for (int p = 1; p < W; ++p) {
+            s.x += v[p].x;
+            s.y += v[p].y;
+        }
+        out[i] = s;
+    }
+    xgmi_finish(a, e);
+}
+
 // out[p * n + i] = in_p[i]: n 8-byte words from every rank (the LM head's packed argmax keys).
 template <int W>
 __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allgather_u64_kernel(XgmiArgs a) {
@@ -241,6 +273,14 @@ extern "C" int dlms_xgmi_allreduce_f32(const XgmiArgs* a, hipStream_t stream) {
     if (a->n % 4) return (int)hipErrorInvalidValue;
     const int grid = xgmi_blocks(a->n / 4);
     XGMI_DISPATCH(xgmi_allreduce_f32_kernel, a->world, grid, *a, stream);
+    return (int)hipGetLastError();
+}
+
+extern "C" int dlms_xgmi_allreduce_i64(const XgmiArgs* a, hipStream_t stream) {
+    if (int r = xgmi_check(a, a->n * 8)) return r;
+    if (a->n % 2) return (int)hipErrorInvalidValue;
+    const int grid = xgmi_blocks(a->n / 2);
+    XGMI_DISPATCH(xgmi_allreduce_i64_kernel, a->world, grid, *a, stream);
     return (int)hipGetLastError();
 }
 

@@ -8,9 +8,13 @@ contiguous region of ``packed`` into an LDS ring; phases hand off through fresh-
 counters and tagged granules in ``scratch``.  See the kernel file for the protocol.
 
 Work split over G CUs (``assign``; pure Python so CPU tests check it):
-  * W_qkv rows (3d), c_fc/c_proj pairs (4d) and LM-head rows (padded vocab) split evenly;
-  * each head's attention runs on ``GS`` CUs, each owning 64/GS head dims of W_o^T (so the
-    out-projection is an axpy of those rows by the head's attention output).
+  * W_qkv rows (3d) and LM-head rows (padded vocab) split evenly;
+  * the MLP in G / J intermediate slices, each on J CUs that publish 1/J of the c_proj outputs;
+  * each head's attention on ``GS`` CUs, each publishing 1/GS of the W_o outputs.
+Why the output partitions (round 4): the r3 in-kernel trace (profiles/r3_df_trace_g200_gs2.json)
+put the granule edge at 0.27 us of a 19.1 us layer but each residual PUBLISH at 0.92 us and the
+two residual edges at 2.9-3.4 us -- the 64-bit counted atomics are issue- and memory-side-bound,
+so the fewer residual words a CU adds, the shorter both the publish and the edge behind it.
 """
 from __future__ import annotations
 
@@ -27,10 +31,9 @@ P = ctypes.c_void_p
 
 
 class DfCu(ctypes.Structure):
-    _fields_ = [("q0", ctypes.c_int), ("nq", ctypes.c_int), ("f0", ctypes.c_int), ("nf", ctypes.c_int),
-                ("v0", ctypes.c_int), ("nv", ctypes.c_int), ("ah", ctypes.c_int), ("ak0", ctypes.c_int),
-                ("nk", ctypes.c_int), ("pad0", ctypes.c_int), ("pad1", ctypes.c_int), ("pad2", ctypes.c_int),
-                ("off", ctypes.c_longlong), ("step_bytes", ctypes.c_longlong)]
+    _fields_ = [(n, ctypes.c_int) for n in ("q0", "nq", "f0", "nf", "v0", "nv", "ah", "ao0", "aon", "pd0", "pdn", "acp",
+                                            "mcp", "pad")] + \
+               [("off", ctypes.c_longlong), ("step_bytes", ctypes.c_longlong)]
 
 
 class DfLayer(ctypes.Structure):
@@ -52,7 +55,7 @@ class DfArgs(ctypes.Structure):
 
 
 LDS_MAX = 160 * 1024
-SUPPORTED_D = (128, 256, 768, 1024)  # larger d: the per-CU MLP region outgrows the ring (round 4)
+SUPPORTED_D = (128, 256, 768, 1024, 1280, 1600)  # GPT-2 small / medium / large / XL (+ tiny test widths)
 MAX_ROWS = 2
 ERRORS = {1: "arrival-counter wait timed out", 2: "q/k/v granule wait timed out", 3: "LDS hand-off wait timed out",
           4: "weight loader timed out", 5: "injected fault (test hook)"}
@@ -103,52 +106,77 @@ class CuPlan:
     nf: int
     v0: int
     nv: int
-    ah: int = -1
-    ak0: int = 0
-    nk: int = 0
+    pd0: int = 0      # c_proj output columns [pd0, pd0 + pdn) of this CU's intermediate slice
+    pdn: int = 0
+    mcp: int = 0      # residual copy its MLP contributions go to
+    ah: int = -1      # attention head (-1: none) ...
+    ao0: int = 0      # ... and its W_o output columns [ao0, ao0 + aon) (all 64 head dims)
+    aon: int = 0
+    acp: int = 0      # residual copy its attention contributions go to
 
     def layer_elems(self, d: int, ko: int, kf: int) -> int:
         """bf16 elements of one layer in the stream: W_qkv rows (padded), the K-major W_o block
-        [d][ko] (attention CUs), the c_fc rows (padded), the K-major c_proj block [d][kf]."""
-        return (self.nq + self.nf) * (d + ROW_PAD) + (d * ko if self.nk else 0) + d * kf
+        [aon][ko] (attention CUs), the c_fc rows (padded), the K-major c_proj block [pdn][kf]."""
+        return (self.nq + self.nf) * (d + ROW_PAD) + (self.aon * ko if self.ah >= 0 else 0) + self.pdn * kf
 
     def step_elems(self, L: int, d: int, ko: int, kf: int) -> int:
         return L * self.layer_elems(d, ko, kf) + self.nv * (d + ROW_PAD)
 
 
 def block_k(cus: list[CuPlan]) -> tuple[int, int]:
-    """(ko, kf): K of the W_o / c_proj blocks, padded to the 16-deep MFMA step (same for all CUs)."""
-    nk = max((cu.nk for cu in cus), default=0)
-    return pad16(nk), pad16(max(cu.nf for cu in cus))
+    """(ko, kf): K of the W_o / c_proj blocks, padded to the 16-deep MFMA step (same for all CUs):
+    a W_o block holds all 64 dims of its head."""
+    return 64, pad16(max(cu.nf for cu in cus))
 
 
-def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int) -> list[CuPlan]:
-    """Work of each of G CUs (see module docstring).  Attention CU a = h * GS + g sits at CU
-    (a * G) // A, spreading the A = n_head * GS attention CUs over all XCDs."""
-    if 64 % GS or n_head * GS > G:
-        raise ValueError(f"dataflow: GS={GS} must divide 64 and n_head * GS <= {G}")
+def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int, J: int = 1,
+           copies: int = 2) -> list[CuPlan]:
+    """Work of each of G CUs (see module docstring).
+
+    * W_qkv rows and LM-head rows: split evenly over the G CUs.
+    * MLP: the intermediate columns are split into I = G / J slices; the J CUs of a slice each
+      compute its c_fc rows (the same h) and publish c_proj for 1/J of the output columns -- so a
+      CU adds d / J residual words per row instead of d (the per-CU atomic issue and the memory-side
+      atomic count of the post-MLP edge shrink J-fold; the extra c_fc rows are prefetched weight
+      bytes, off the critical path).  Slice i's contributions go to residual copy i % copies.
+    * Attention: each head on GS CUs; each computes the whole head and publishes its W_o output
+      columns [g d/GS, (g + 1) d/GS) (d / GS words instead of d), into copy h % copies.
+      Attention CU a = h * GS + g sits at CU (a * G) // A, spreading them over all XCDs.
+    Every residual word then receives exactly I contributions after the MLP (n_head after the
+    attention), split over the copies the same way for every word."""
+    if n_head * GS > G or d % (16 * GS):
+        raise ValueError(f"dataflow: GS={GS}: need n_head * GS <= {G} and d % (16 GS) == 0")
+    if G % J or d % (16 * J):
+        raise ValueError(f"dataflow: J={J} must divide G={G} and d / J must be a multiple of 16")
+    I = G // J
+    if I > n_inner:
+        raise ValueError("dataflow: more MLP slices than intermediate columns")
     cus = []
     for c in range(G):
         q0, nq = split_even(3 * d, G, c)
-        f0, nf = split_even(n_inner, G, c)
+        i, j = divmod(c, J)
+        f0, nf = split_even(n_inner, I, i)
         v0, nv = split_even(vocab_padded, G, c)
-        cus.append(CuPlan(q0, nq, f0, nf, v0, nv))
+        cus.append(CuPlan(q0, nq, f0, nf, v0, nv, pd0=j * (d // J), pdn=d // J, mcp=i % copies))
     A = n_head * GS
-    nk = 64 // GS
     for a in range(A):
         cu = cus[(a * G) // A]
-        cu.ah, cu.ak0, cu.nk = a // GS, (a % GS) * nk, nk
+        h, g = divmod(a, GS)
+        cu.ah, cu.ao0, cu.aon, cu.acp = h, g * (d // GS), d // GS, h % copies
     return cus
 
 
-def kmajor_blocks(w: torch.Tensor, cols: list[list[int]], K: int) -> torch.Tensor:
-    """w [d, n] -> [len(cols), d, K]: block c = w[:, cols[c]] zero-padded to K columns."""
-    d = w.shape[0]
-    ext = torch.cat([w, torch.zeros(d, 1, dtype=w.dtype, device=w.device)], dim=1)
-    idx = torch.full((len(cols), K), w.shape[1], dtype=torch.long)
-    for c, cc in enumerate(cols):
-        idx[c, : len(cc)] = torch.tensor(cc, dtype=torch.long)
-    return ext[:, idx.to(w.device).reshape(-1)].reshape(d, len(cols), K).permute(1, 0, 2).contiguous()
+def expected_contributions(cus: list[CuPlan], copies: int) -> tuple[list[int], list[int]]:
+    """(attention, MLP) contributions each residual copy's words receive (the same for every word)."""
+    att = [0] * copies
+    for cu in cus:
+        if cu.ah >= 0 and cu.ao0 == 0:  # one CU per head covers any given column; count column 0's
+            att[cu.acp] += 1
+    mlp = [0] * copies
+    for cu in cus:
+        if cu.pd0 == 0:
+            mlp[cu.mcp] += 1
+    return att, mlp
 
 
 def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]:
@@ -158,23 +186,22 @@ def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]
     cfg = w.cfg
     d, L = cfg.n_embd, cfg.n_layer
     ko, kf = block_k(cus)
-    G = len(cus)
     sizes = [cu.step_elems(L, d, ko, kf) for cu in cus]
     starts = np.cumsum([0] + sizes)[:-1].tolist()
     packed = torch.zeros(sum(sizes), dtype=torch.bfloat16, device=device)
     pad = lambda t: torch.nn.functional.pad(t, (0, ROW_PAD))  # noqa: E731
-    o_cols = [[cu.ah * 64 + cu.ak0 + k for k in range(cu.nk)] for cu in cus]
-    p_cols = [[cu.f0 + i for i in range(cu.nf)] for cu in cus]
     for l, lw in enumerate(w.layers):
         qkv, fc = pad(lw.w_qkv), pad(lw.w_fc)
-        ob = kmajor_blocks(lw.w_o, o_cols, ko).reshape(G, -1)
-        pb = kmajor_blocks(lw.w_p, p_cols, kf).reshape(G, -1)
         for c, cu in enumerate(cus):
             o = starts[c] + l * cu.layer_elems(d, ko, kf)
-            for piece in (qkv[cu.q0: cu.q0 + cu.nq].reshape(-1), ob[c] if cu.nk else None,
-                          fc[cu.f0: cu.f0 + cu.nf].reshape(-1), pb[c]):
-                if piece is None:
-                    continue
+            pieces = [qkv[cu.q0: cu.q0 + cu.nq].reshape(-1)]
+            if cu.ah >= 0:  # W_o[out, in]: outputs [ao0, +aon) x the head's 64 input dims
+                pieces.append(lw.w_o[cu.ao0: cu.ao0 + cu.aon, cu.ah * 64: cu.ah * 64 + 64].reshape(-1))
+            pieces.append(fc[cu.f0: cu.f0 + cu.nf].reshape(-1))
+            blk = torch.zeros(cu.pdn, kf, dtype=torch.bfloat16, device=device)
+            blk[:, : cu.nf] = lw.w_p[cu.pd0: cu.pd0 + cu.pdn, cu.f0: cu.f0 + cu.nf]
+            pieces.append(blk.reshape(-1))
+            for piece in pieces:
                 packed[o: o + piece.numel()].copy_(piece)
                 o += piece.numel()
     lm = pad(w.wte)
@@ -185,12 +212,15 @@ def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]
 
 
 def ring_window(cus: list[CuPlan], d: int, ko: int, kf: int, nc: int = 4) -> int:
-    """``DataflowDecoder.ring_window`` for a plan (bytes)."""
+    """``DataflowDecoder.ring_window`` for a plan (bytes): the largest piece of the stream some
+    compute wave needs resident at once beyond what every wave has released -- the QKV rows, the
+    W_o block, the c_fc rows, the c_proj block (the c_fc rows are released before the wait for it)
+    or one 16-row LM-head group (each wave releases everything before its next group first)."""
     rowb = 2 * d + 32
     need = 0
     for cu in cus:
-        need = max(need, cu.nq * rowb, d * ko * 2 if cu.nk else 0, cu.nf * rowb + d * kf * 2,
-                   min(cu.nv, nc * 16) * rowb)
+        need = max(need, cu.nq * rowb, cu.aon * ko * 2 if cu.ah >= 0 else 0, cu.nf * rowb, cu.pdn * kf * 2,
+                   min(cu.nv, 16) * rowb)
     return need
 
 
@@ -204,11 +234,11 @@ class DataflowDecoder:
         return (eng.tp_size == 1 and not eng.w.fp8 and cfg.n_embd in SUPPORTED_D and cfg.n_embd == 64 * cfg.n_head
                 and eng.w.ffn_local == 4 * cfg.n_embd)
 
-    def __init__(self, eng, grid: int | None = None, gs: int | None = None):
+    def __init__(self, eng, grid: int | None = None, gs: int | None = None, j: int | None = None):
         if not self.supported(eng):
             raise ValueError("dataflow decode: TP=1 bf16 GPT-2 with d in %s only" % (SUPPORTED_D,))
         self.L = _bind_once()
-        self.COPIES = int(self.L.dlms_df_copies())  # fixed-point residual copies (CU c adds into copy c % COPIES)
+        self.COPIES = int(self.L.dlms_df_copies())  # fixed-point residual copies (assign(): acp / mcp)
         self.eng = eng
         cfg, dev = eng.cfg, eng.device
         props = torch.cuda.get_device_properties(dev)
@@ -219,10 +249,15 @@ class DataflowDecoder:
         cus = int(props.multi_processor_count)
         G = grid or int(os.environ.get("DLMS_DF_GRID", "0")) or min(cus * 25 // 32, 256)
         gs = gs or int(os.environ.get("DLMS_DF_GS", "2"))
-        while cfg.n_head * gs > G and gs > 1:
+        while (cfg.n_head * gs > G or cfg.n_embd % (16 * gs)) and gs > 1:
             gs //= 2
-        self.G, self.GS = G, gs
-        self.cus = assign(cfg.n_embd, cfg.n_head, eng.w.ffn_local, cfg.vocab_padded, G, gs)
+        # MLP output groups J (see assign): as many as keep a slice's c_fc rows <= 64 and the
+        # largest stream piece inside the ring -- 4 at d 768, 2 at 1024, 1 for large / XL
+        j = j or int(os.environ.get("DLMS_DF_J", "0")) or {768: 4, 1024: 2}.get(cfg.n_embd, 1)
+        while j > 1 and (G % j or -(-eng.w.ffn_local * j // G) > 64 or cfg.n_embd % (16 * j)):
+            j -= 1
+        self.G, self.GS, self.J = G, gs, j
+        self.cus = assign(cfg.n_embd, cfg.n_head, eng.w.ffn_local, cfg.vocab_padded, G, gs, j, self.COPIES)
         self.A = cfg.n_head * gs
         self.ko, self.kf = block_k(self.cus)
         if self.ko > 64 or self.kf > 64:
@@ -236,8 +271,8 @@ class DataflowDecoder:
         self.swl = -(-max_nv // 64) * 2 + 2
         tab = (DfCu * G)()
         for c, cu in enumerate(self.cus):
-            tab[c] = DfCu(cu.q0, cu.nq, cu.f0, cu.nf, cu.v0, cu.nv, cu.ah, cu.ak0, cu.nk, 0, 0, 0,
-                          starts[c] * 2, cu.step_elems(cfg.n_layer, D, self.ko, self.kf) * 2)
+            tab[c] = DfCu(cu.q0, cu.nq, cu.f0, cu.nf, cu.v0, cu.nv, cu.ah, cu.ao0, cu.aon, cu.pd0, cu.pdn, cu.acp,
+                          cu.mcp, 0, starts[c] * 2, cu.step_elems(cfg.n_layer, D, self.ko, self.kf) * 2)
         self.max_step_bytes = max(cu.step_elems(cfg.n_layer, D, self.ko, self.kf) for cu in self.cus) * 2
         self.cu_tab = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
         lt = (DfLayer * cfg.n_layer)()
@@ -254,9 +289,7 @@ class DataflowDecoder:
         # per-launch constants (the continuous batcher launches once per decode chunk)
         self._ring_bytes = {R: self._ring_bytes_for(R) for R in range(1, MAX_ROWS + 1)}
         self._window = ring_window(self.cus, cfg.n_embd, self.ko, self.kf, self.NC)
-        self._exp_mlp = [sum(1 for i in range(G) if i % self.COPIES == c) for c in range(self.COPIES)]
-        self._exp_att = [sum(1 for i, cu in enumerate(self.cus) if cu.nk and i % self.COPIES == c)
-                         for c in range(self.COPIES)]
+        self._exp_att, self._exp_mlp = expected_contributions(self.cus, self.COPIES)
         # cooperative launch (the runtime guarantees the grid is co-resident); DLMS_DF_COOP=0: plain
         self.coop = os.environ.get("DLMS_DF_COOP", "1") != "0"
         self._fault_step = -1
@@ -279,11 +312,10 @@ class DataflowDecoder:
 
     def ring_window(self) -> int:
         """The most stream bytes a compute wave needs resident beyond the slowest wave's released
-        prefix (every wait in dataflow.hip's compute_wave): the QKV rows; the W_o block; the c_fc
-        rows + the c_proj block (consumed together); and, for the LM head's 16-row groups dealt
-        round-robin to the NC waves, NC groups.  The loader only fetches whole 8 KiB batches that
-        fit behind that prefix, so a launch needs ``ring_window() + BATCH <= ring_bytes`` or a wave
-        would wait forever for bytes the loader may not fetch (caught as a hand-off timeout)."""
+        prefix (every wait in dataflow.hip's compute_wave; see ``ring_window`` above).  The loader
+        only fetches whole 8 KiB batches that fit behind that prefix, so a launch needs
+        ``ring_window() + BATCH <= ring_bytes`` or a wave would wait forever for bytes the loader
+        may not fetch (caught as a hand-off timeout)."""
         return self._window
 
     def fits(self, R: int) -> bool:

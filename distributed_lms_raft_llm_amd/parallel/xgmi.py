@@ -78,6 +78,20 @@ class XgmiComm:
         ops._check(ops.lib().dlms_xgmi_allreduce_f32(ctypes.byref(a), ops._stream()), "dlms_xgmi_allreduce_f32")
         return t
 
+    def all_reduce_i64_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place integer sum over the group of a contiguous int64 tensor (even numel): the TP
+        fused decode's fixed-point residual partials (exact, identical on every rank)."""
+        ops._req(t, torch.int64, "t")
+        if not t.is_contiguous() or t.numel() % 2:
+            raise ValueError("xgmi all_reduce_i64_: contiguous int64 with an even numel")
+        if t.numel() * 8 > self.slab_bytes:
+            raise ValueError(f"xgmi all_reduce_i64_: {t.numel() * 8} B exceeds the {self.slab_bytes} B slab")
+        if t.device != self.device:
+            raise ValueError("xgmi all_reduce_i64_: tensor on another device")
+        a = self._args(t, t, t.numel())
+        ops._check(ops.lib().dlms_xgmi_allreduce_i64(ctypes.byref(a), ops._stream()), "dlms_xgmi_allreduce_i64")
+        return t
+
     def all_gather_u64(self, src: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """``out[p] = src`` of rank p, for 8-byte elements (int64 packed argmax keys)."""
         ops._req(src, torch.int64, "src", 1)

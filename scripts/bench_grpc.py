@@ -365,6 +365,9 @@ def main():
             m0, w0 = metrics(tutor_addr), time.time()
             time.sleep(max(0.0, t_stop - time.time()))
             m1, w1 = metrics(tutor_addr), time.time()
+            # the LMS nodes' own view (gate batching, the whole GetLLMAnswer, tutor failovers): where
+            # the LMS path's latency goes beyond the tutoring tier's
+            lms_m = {a: metrics(a) for a in addrs} if args.target == "lms" else {}
             results = [conn.recv() for _, conn in clients]
             recs = [r for rr, _ in results for r in rr]
             win = [r for r in recs if t_meas <= r[0] < t_stop]
@@ -405,6 +408,11 @@ def main():
                            if k in hist},
                 "boot_s": round(boot_s, 1),
             }
+            if lms_m:
+                line["lms_nodes"] = {
+                    a: {k: {q: round(v, 2) for q, v in m.get("histograms", {})[k].items() if q in ("count", "p50", "p99")}
+                        for k in ("gate_ms", "llm_answer_ms") if k in m.get("histograms", {})}
+                    for a, m in lms_m.items()}
             print(json.dumps(line), flush=True)
             if args.out:
                 with open(args.out, "a") as f:

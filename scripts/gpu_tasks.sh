@@ -20,6 +20,7 @@
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
+#   grpc:<tgt>:<rates> scripts/bench_grpc.py --target tutoring|lms at those offered q/s -> gpurun_out/grpc.jsonl
 #   e2e:<n>          scripts/run_config.py --config n (Raft cluster + gate + tutor) -> gpurun_out/e2e_<n>.log
 #   e2e1:<n>         the same with the tutor at TP=1 (one-GPU boxes: configs 4/5 ask for TP=4/8)
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
@@ -57,6 +58,9 @@ prof() {  # prof <tag> <bench args...>
 for task in "$@"; do
     case "$task" in
         tests) step 900 gpurun_out/tests.log $T -m gpu tests/; tail -2 gpurun_out/tests.log ;;
+        testall:*)  # the same without -x: every failure of the selection is reported (the call still ends on it)
+            step 900 gpurun_out/test_all.log python -u -m pytest -q -rf --timeout 180 --timeout-method thread -m gpu \
+                ${task#testall:}; tail -2 gpurun_out/test_all.log ;;
         test:*) step 600 gpurun_out/test_sel.log $T -m gpu ${task#test:}; tail -2 gpurun_out/test_sel.log ;;
         testenv:*)  # testenv:<ENV=v>:<paths>  one gpu test selection under an environment setting
             spec=${task#testenv:}; envs=${spec%%:*}; paths=${spec#*:}
@@ -103,6 +107,15 @@ for task in "$@"; do
                       --modes continuous --prompt-jitter 0; grep '^{' gpurun_out/serving5.jsonl ;;
         serving) step 400 gpurun_out/serving.jsonl python -u scripts/bench_serving.py --rates 20,200,1000 --queries 400 \
                      --modes continuous; grep '^{' gpurun_out/serving.jsonl ;;
+        dfsweep:*)  # dfsweep:<df_sweep.sh args, ';' for spaces>  e.g. dfsweep:-b;1,2;default;DLMS_DF_J=1
+            spec=${task#dfsweep:}
+            step 900 gpurun_out/dfsweep.log bash scripts/df_sweep.sh -o gpurun_out/df_sweep.jsonl ${spec//;/ }
+            tail -12 gpurun_out/dfsweep.log ;;
+        grpc:*)  # grpc:<tutoring|lms>:<rates>  sustained open-loop gRPC serving -> gpurun_out/grpc.jsonl
+            spec=${task#grpc:}; tgt=${spec%%:*}; rates=${spec#*:}
+            step 600 gpurun_out/grpc.log python -u scripts/bench_grpc.py --target "$tgt" --rates "$rates" --duration 20 \
+                --warmup 8 --client-procs 8 --out gpurun_out/grpc.jsonl --log gpurun_out/grpc_server.log
+            tail -2 gpurun_out/grpc.jsonl | cut -c1-400 ;;
         e2e:*) step 900 gpurun_out/e2e_${task#e2e:}.log python -u scripts/run_config.py --config ${task#e2e:}
                tail -3 gpurun_out/e2e_${task#e2e:}.log ;;
         e2e1:*) step 900 gpurun_out/e2e_${task#e2e1:}_tp1.log python -u scripts/run_config.py --config ${task#e2e1:} --tp 1

@@ -63,7 +63,8 @@ def _oracle(cfg, w, outs, prompts, eps=0.05):
 
 @pytest.mark.parametrize("name,T,lens", [("gpt2-tiny", 64, [9]), ("gpt2-tiny", 64, [9, 20]),
                                          ("gpt2", 150, [32]), ("gpt2", 150, [32, 17]),
-                                         ("gpt2-medium", 80, [24])])
+                                         ("gpt2-medium", 80, [24]), ("gpt2-large", 80, [24]),
+                                         ("gpt2-xl", 64, [16]), ("gpt2-xl", 64, [16, 5])])
 def test_dataflow_matches_fp32_oracle(name, T, lens):
     cfg, w = _setup(name)
     eng = _engine(cfg, w, True, max_batch=2, max_length=T)

@@ -9,34 +9,55 @@ from distributed_lms_raft_llm_amd.models.config import GPT2Config, gpt2_config
 from distributed_lms_raft_llm_amd.ops.dataflow import ROW_PAD, assign, block_k, pack_weights
 
 
-@pytest.mark.parametrize("name,G,GS", [("gpt2", 256, 4), ("gpt2-medium", 256, 4), ("gpt2-xl", 256, 4),
-                                       ("gpt2-tiny", 64, 4), ("gpt2", 80, 2)])
-def test_assignment_covers_every_row_once(name, G, GS):
+@pytest.mark.parametrize("name,G,GS,J", [("gpt2", 256, 4, 1), ("gpt2", 200, 2, 4), ("gpt2-medium", 200, 2, 2),
+                                         ("gpt2-xl", 256, 4, 1), ("gpt2-xl", 200, 2, 1), ("gpt2-large", 200, 2, 1),
+                                         ("gpt2-tiny", 64, 4, 2), ("gpt2", 80, 2, 1)])
+def test_assignment_covers_every_row_once(name, G, GS, J):
+    """Every W_qkv row and LM-head row on exactly one CU; every (intermediate column, output column)
+    pair of c_proj on exactly one CU (the J CUs of a slice split its outputs); every (head, output
+    column) of W_o on exactly one attention CU; and the per-copy contribution counts the kernel
+    polls for hold for EVERY residual word."""
+    from distributed_lms_raft_llm_amd.ops.dataflow import expected_contributions
+
     cfg = gpt2_config(name)
     d, H, F, V = cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded
-    cus = assign(d, H, F, V, G, GS)
+    C = 2
+    cus = assign(d, H, F, V, G, GS, J, C)
     assert len(cus) == G
-    for key, n in (("q", 3 * d), ("f", F), ("v", V)):
+    for key, n in (("q", 3 * d), ("v", V)):
         covered = np.zeros(n, dtype=int)
         for cu in cus:
             s, c = getattr(cu, key + "0"), getattr(cu, "n" + key)
             covered[s: s + c] += 1
         assert (covered == 1).all(), key
-    # W_o^T rows: head h, dims [ak0, ak0 + nk) -- every (head, dim) exactly once
-    cov = np.zeros((H, 64), dtype=int)
+    cp = np.zeros((F, d), dtype=int)
+    per_word = np.zeros((C, d), dtype=int)
+    for cu in cus:
+        cp[cu.f0: cu.f0 + cu.nf, cu.pd0: cu.pd0 + cu.pdn] += 1
+        per_word[cu.mcp, cu.pd0: cu.pd0 + cu.pdn] += 1
+    assert (cp == 1).all()
+    cov = np.zeros((H, d), dtype=int)
+    att_word = np.zeros((C, d), dtype=int)
     att = [cu for cu in cus if cu.ah >= 0]
     assert len(att) == H * GS
     for cu in att:
-        cov[cu.ah, cu.ak0: cu.ak0 + cu.nk] += 1
+        cov[cu.ah, cu.ao0: cu.ao0 + cu.aon] += 1
+        att_word[cu.acp, cu.ao0: cu.ao0 + cu.aon] += 1
     assert (cov == 1).all()
-    assert max(cu.nq for cu in cus) <= 64
+    exp_att, exp_mlp = expected_contributions(cus, C)
+    for c in range(C):
+        assert (att_word[c] == exp_att[c]).all() and (per_word[c] == exp_mlp[c]).all()
+    assert sum(exp_att) == H and sum(exp_mlp) == G // J
+    assert max(cu.nq for cu in cus) <= 64 and max(cu.nf for cu in cus) <= 64
 
 
 def test_assignment_rejects_bad_split():
     with pytest.raises(ValueError):
         assign(768, 12, 3072, 50304, 16, 4)  # 48 attention CUs on 16
     with pytest.raises(ValueError):
-        assign(768, 12, 3072, 50304, 256, 3)  # 3 does not divide 64
+        assign(768, 12, 3072, 50304, 256, 5)  # 768 / 5 output columns: not a multiple of 16
+    with pytest.raises(ValueError):
+        assign(768, 12, 3072, 50304, 200, 2, 3)  # J must divide G
 
 
 def test_packed_stream_matches_sources():
@@ -45,8 +66,8 @@ def test_packed_stream_matches_sources():
 
     cfg = GPT2Config("df-test", n_layer=2, n_embd=128, n_head=2, n_positions=64, vocab_size=300, eos_token_id=299)
     w = prepare_gpt2_weights(cfg, init_gpt2_weights(cfg, seed=3), "cpu")
-    G, GS = 16, 4
-    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, GS)
+    G, GS, J = 16, 4, 2
+    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, GS, J)
     packed, starts = pack_weights(w, cus, "cpu")
     ko, kf = block_k(cus)
     d, L = cfg.n_embd, cfg.n_layer
@@ -63,16 +84,16 @@ def test_packed_stream_matches_sources():
         for l, lw in enumerate(w.layers):
             assert torch.equal(rows(o, cu.nq), lw.w_qkv[cu.q0: cu.q0 + cu.nq])
             o += cu.nq * (d + ROW_PAD)
-            if cu.nk:
-                blk = packed[o: o + d * ko].reshape(d, ko)  # K-major: [d][ko]
-                cols = lw.w_o[:, cu.ah * 64 + cu.ak0: cu.ah * 64 + cu.ak0 + cu.nk]
-                assert torch.equal(blk[:, : cu.nk], cols) and not blk[:, cu.nk:].any()
-                o += d * ko
+            if cu.ah >= 0:
+                blk = packed[o: o + cu.aon * ko].reshape(cu.aon, ko)  # K-major: [outputs][64 head dims]
+                assert torch.equal(blk, lw.w_o[cu.ao0: cu.ao0 + cu.aon, cu.ah * 64: cu.ah * 64 + 64])
+                o += cu.aon * ko
             assert torch.equal(rows(o, cu.nf), lw.w_fc[cu.f0: cu.f0 + cu.nf])
             o += cu.nf * (d + ROW_PAD)
-            blk = packed[o: o + d * kf].reshape(d, kf)
-            assert torch.equal(blk[:, : cu.nf], lw.w_p[:, cu.f0: cu.f0 + cu.nf]) and not blk[:, cu.nf:].any()
-            o += d * kf
+            blk = packed[o: o + cu.pdn * kf].reshape(cu.pdn, kf)
+            want = lw.w_p[cu.pd0: cu.pd0 + cu.pdn, cu.f0: cu.f0 + cu.nf]
+            assert torch.equal(blk[:, : cu.nf], want) and not blk[:, cu.nf:].any()
+            o += cu.pdn * kf
         assert torch.equal(rows(o, cu.nv), w.wte[cu.v0: cu.v0 + cu.nv])
 
 
@@ -102,9 +123,8 @@ def _emulate_step(cfg, w, cus, tok, pos, kv):
             K = torch.cat([f(kv[l][0][hh]), qkv[d + hh * 64: d + (hh + 1) * 64][None]])
             V = torch.cat([f(kv[l][1][hh]), qkv[2 * d + hh * 64: 2 * d + (hh + 1) * 64][None]])
             p = torch.softmax(K @ q / 8.0, dim=0)
-            o = p @ V
-            for k in range(cu.nk):  # axpy of this CU's W_o^T rows
-                xa += o[cu.ak0 + k] * f(lw.w_o[:, hh * 64 + cu.ak0 + k])
+            o = p @ V  # the whole head; this CU adds W_o for its output columns only
+            xa[cu.ao0: cu.ao0 + cu.aon] += f(lw.w_o[cu.ao0: cu.ao0 + cu.aon, hh * 64:(hh + 1) * 64]) @ o
         h2 = ln(xa, lw.ln2_g, lw.ln2_b)
         xm = xa + f(lw.b_p)
         for cu in cus:
@@ -112,7 +132,7 @@ def _emulate_step(cfg, w, cus, tok, pos, kv):
                 j = cu.f0 + i
                 a = f(lw.w_fc[j]) @ h2 + f(lw.b_fc[j])
                 g = 0.5 * a * (1 + torch.tanh(0.7978845608028654 * (a + 0.044715 * a ** 3)))
-                xm += g * f(lw.w_p[:, j])
+                xm[cu.pd0: cu.pd0 + cu.pdn] += g * f(lw.w_p[cu.pd0: cu.pd0 + cu.pdn, j])
         x = xm
     return ln(x, w.lnf_g, w.lnf_b)
 
@@ -127,7 +147,7 @@ def test_split_reproduces_the_reference_step():
     raw = init_gpt2_weights(cfg, seed=5)
     perturb_norms_and_biases(raw)
     w = prepare_gpt2_weights(cfg, raw, "cpu", dtype=torch.float32)
-    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, 8, 2)
+    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, 8, 2, 2)
     ref = GPT2Reference(cfg, raw, device="cpu", dtype=torch.float64)
     seq = [5, 17, 42, 7]
     cache = KVCache.allocate(cfg, 1, 8, dtype=torch.float64, device="cpu")
@@ -139,22 +159,25 @@ def test_split_reproduces_the_reference_step():
     torch.testing.assert_close(got, hid[-1].double(), atol=1e-6, rtol=1e-6)
 
 
-@pytest.mark.parametrize("name,G,window", [
-    ("gpt2", 256, 4 * 16 * 1568),            # the LM head's NC in-flight 16-row groups
-    ("gpt2-medium", 256, 4 * 16 * 2080),     # 133 KiB: fits the 144 KiB ring at 1 row only
-    ("gpt2-medium", 128, 4 * 16 * 2080),     # ... and its c_fc rows + c_proj block need 132096 B
+@pytest.mark.parametrize("name,G,GS,window", [
+    ("gpt2", 256, 4, 16 * 1568),             # one 16-row LM-head group (waves release ahead of it)
+    ("gpt2-medium", 256, 4, 16 * 2080),      # c_fc rows and LM-head group tie
+    ("gpt2-medium", 128, 4, 32 * 2080),      # 32 c_fc rows (the c_proj block no longer adds to them)
+    ("gpt2-large", 200, 2, 1280 * 32 * 2),   # the W_o / c_proj blocks, K padded to 32
+    ("gpt2-xl", 200, 2, 32 * 3232),          # 32 c_fc rows of 3.2 KB
 ])
-def test_ring_window(name, G, window):
-    """The stream window a compute wave needs resident (ops/dataflow.py ring_window): the
-    gpt2-medium launches that stalled on the GPU (profiles/r3_df_hang_probe.jsonl) are exactly
-    those whose window + one 8 KiB loader batch exceeds the ring."""
+def test_ring_window(name, G, GS, window):
+    """The stream window a compute wave needs resident (ops/dataflow.py ring_window).  The
+    c_fc rows are released before the wait for the c_proj block and each LM-head wave releases
+    everything before its next group, so the window is the largest SINGLE piece: GPT-2-large
+    and XL now fit the ring (the old "c_fc + c_proj together, NC LM-head groups" rule needed
+    150-207 KB there), with the one 8 KiB loader batch of slack every launch needs."""
     from distributed_lms_raft_llm_amd.ops.dataflow import ring_window
 
     cfg = gpt2_config(name)
-    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, 4)
+    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, GS)
     ko, kf = block_k(cus)
     assert ring_window(cus, cfg.n_embd, ko, kf) == window
-    if G == 128:  # the r3 loader stall at layer 4: the MLP window alone overflows the old ring
-        assert max(cu.nf for cu in cus) * 2080 + cfg.n_embd * kf * 2 + 8192 > 139264
-    # the r3 probe: medium at 256 CUs with the old 139264 B ring (hb staged 16 rows) stalls
-    assert ring_window(cus, cfg.n_embd, ko, kf) + 8192 > 139264 or name == "gpt2"
+    # 139264 B: the smallest ring any supported width gets at one row (160 KiB minus the fixed
+    # LDS areas, rounded down to the 8 KiB loader batch)
+    assert ring_window(cus, cfg.n_embd, ko, kf) + 8192 <= 139264

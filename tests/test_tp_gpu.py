@@ -58,6 +58,13 @@ def _worker(rank, world, port, q, p2p=False, geo="tp5"):
         assert (eng.xgmi is not None) == p2p
         hid = eng.prefill_last_hidden(prompts).cpu()
         out = eng.generate(prompts)
+        fused = eng.tp_fused_steps
+        if geo in ("large", "xl"):  # configs 4 / 5: the six-kernel fused TP layer ran
+            assert eng.tp_fused and fused > 0, (eng.tp_fused, fused)
+        # a second generation of the same shapes: replays the captured prefill (xGMI) -- same tokens
+        assert eng.generate(prompts) == out
+        if p2p:
+            assert any(st["graph"] is not None for st in eng._pgraphs.values()), "no TP prefill graph"
         q.put((rank, eng.w.head_range, hid.numpy(), out, eng.w.ffn_range))
     finally:
         dist.destroy_process_group()
