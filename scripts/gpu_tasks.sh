@@ -107,6 +107,14 @@ for task in "$@"; do
                       --modes continuous --prompt-jitter 0; grep '^{' gpurun_out/serving5.jsonl ;;
         serving) step 400 gpurun_out/serving.jsonl python -u scripts/bench_serving.py --rates 20,200,1000 --queries 400 \
                      --modes continuous; grep '^{' gpurun_out/serving.jsonl ;;
+        tpprof:*)  # tpprof:<tag>:<model>:<tp>  TP ranks sharing cuda:0 under rocprofv3 (one kernel_stats per rank)
+            spec=${task#tpprof:}; tag=${spec%%:*}; rest=${spec#*:}; model=${rest%%:*}; tpn=${rest#*:}
+            export TMPDIR=/tmp; D=gpurun_out/tpprof_$tag; mkdir -p $D
+            step 600 $D/run.log rocprofv3 --kernel-trace --stats -d $D -o run_%pid% --output-format csv \
+                -- python3 scripts/tp_shared_gpu.py --model "$model" --tp "$tpn" --batch 1 --reps 2
+            find $D -name "*_kernel_trace.csv" -delete
+            for f in $(find $D -name "*kernel_stats.csv"); do python scripts/kstats.py "$f" > "${f%.csv}.summary.txt"; done
+            grep '^{' $D/run.log; head -14 $(find $D -name "*kernel_stats.summary.txt" | head -1) ;;
         dfsweep:*)  # dfsweep:<df_sweep.sh args, ';' for spaces>  e.g. dfsweep:-b;1,2;default;DLMS_DF_J=1
             spec=${task#dfsweep:}
             step 900 gpurun_out/dfsweep.log bash scripts/df_sweep.sh -o gpurun_out/df_sweep.jsonl ${spec//;/ }

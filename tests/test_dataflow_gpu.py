@@ -66,13 +66,16 @@ def _oracle(cfg, w, outs, prompts, eps=0.05):
                                          ("gpt2-medium", 80, [24]), ("gpt2-large", 80, [24]),
                                          ("gpt2-xl", 64, [16]), ("gpt2-xl", 64, [16, 5])])
 def test_dataflow_matches_fp32_oracle(name, T, lens):
+    """No token differs from the fp32 oracle where its top-1/top-2 margin is decisive; and most
+    positions ARE decisive (random-init GPT-2-XL's flatter logits: about 2/3 of them at eps 0.05)."""
     cfg, w = _setup(name)
     eng = _engine(cfg, w, True, max_batch=2, max_length=T)
     prompts = _prompts(cfg, lens)
     outs = eng.generate(prompts, repetition_penalty=1.2)
-    assert eng._df is not None, "the dataflow path did not run"
+    assert eng._df is not None and eng._df.launches >= 1, "the dataflow path did not run"
+    assert eng.df_aborts == 0
     total, decisive = _oracle(cfg, w, outs, prompts)
-    assert total > 0 and decisive >= 0.7 * total, (total, decisive)
+    assert total > 0 and decisive >= (0.6 if name == "gpt2-xl" else 0.7) * total, (total, decisive)
 
 
 @pytest.mark.parametrize("name,T,lens", [("gpt2-tiny", 64, [9]), ("gpt2", 150, [32]), ("gpt2", 150, [32, 40])])
@@ -138,14 +141,15 @@ def _with_eos(cfg, eos):
     return GPT2Config(**d)
 
 
-def _first_new(seq, plen, k0=3):
-    """(index, token) of the first generated token at step >= k0 that did not occur earlier in
-    the generated part: making it the EOS id stops the row exactly there."""
+def _first_new(seq, plen, k0=1):
+    """(index, token) of a generated token at step >= k0 that did not occur earlier in the
+    generated part (the one nearest the middle): making it the EOS id stops the row exactly there."""
     gen = seq[plen:]
-    for k in range(k0, len(gen)):
-        if gen[k] not in gen[:k]:
-            return k, gen[k]
-    raise AssertionError("no usable token")
+    cands = [k for k in range(k0, len(gen)) if gen[k] not in gen[:k]]
+    if not cands:
+        raise AssertionError(f"no usable token in {gen}")
+    k = min(cands, key=lambda c: abs(c - len(gen) // 2))  # as deep into the launch as possible
+    return k, gen[k]
 
 
 @pytest.mark.parametrize("rows", [1, 2])
@@ -158,7 +162,7 @@ def test_dataflow_forced_eos_mid_launch(rows):
     T = 90
     prompts = _prompts(cfg, [20, 9][:rows], seed=11)
     base = _engine(cfg, w, True, max_batch=2, max_length=T).generate(prompts)
-    k, tok = _first_new(base[0], len(prompts[0]), k0=4)
+    k, tok = _first_new(base[0], len(prompts[0]), k0=1)  # (gen[0] is the prefill's token)
     cfg2 = _with_eos(cfg, tok)
     want = []
     for b, (s, p) in enumerate(zip(base, prompts)):
