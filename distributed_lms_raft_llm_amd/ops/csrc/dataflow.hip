@@ -130,15 +130,18 @@ struct Args {
 
 // ------------------------------------------------------------------ LDS layout (host mirrors it)
 struct Lay {
-    int ring, ctl, st, xn, res, part, att, mrg, seen, keys, hb, fcp, total;
+    int ring, ctl, st, xn, res, part, att, mrg, seen, keys, hb, fcp, xs, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
 __host__ __device__ inline Lay lds_layout(int D, int R, int max_nq, int swl, int ring_bytes) {
+    // the small per-CU areas FIRST, the weight ring last: every LDS address the comm / compute
+    // waves form with a constant offset then fits the 16-bit ds_* immediate (with the ring first
+    // they sat above 64 KiB and the compiler kept one address register per unrolled access live
+    // across the step loop -- the two-row kernel spilled to scratch)
     Lay o;
     int off = 0;
-    o.ring = off; off += ring_bytes;
     o.ctl = off; off += 64 * 4;
     o.st = off; off += 8 * R * 4;
     o.xn = off; off = align16(off + R * D * 2);                          // bf16 activation (A fragments)
@@ -150,6 +153,8 @@ __host__ __device__ inline Lay lds_layout(int D, int R, int max_nq, int swl, int
     o.keys = off; off = align16(off + NC * R * 8);
     o.hb = off; off = align16(off + NC * R * 64 * 2);                    // per-wave A staging (bf16 [R][64])
     o.fcp = off; off = align16(off + NC * R * 64 * 4);                   // K-split c_fc partials
+    o.xs = off; off = align16(off + R * D * 8);                          // the comm wave's int64 residual
+    o.ring = off; off += ring_bytes;
     o.total = off;
     return o;
 }
@@ -325,7 +330,7 @@ __device__ __forceinline__ void layer_norm(float (&x)[R][D / 64], const float (&
 // only ever read below its final count.
 template <int D, int R>
 __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const float (&bias)[D / 64],
-                                           i64 (&xs)[R][D / 64], const Args& a, unsigned* ctl, unsigned where, int s,
+                                           i64* xs, const Args& a, unsigned* ctl, unsigned where, int s,
                                            int lane) {
     constexpr int EPL = D / 64;
     const __amdgpu_buffer_rsrc_t rs =
@@ -385,7 +390,7 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
                     i64 t = f2fix(bias[i]);
 #pragma unroll
                     for (int c = 0; c < COPIES; ++c) t += (i64)(v[c][r][i] & CNT_MASK) - (i64)ec[c] * CNT_BIAS;
-                    xs[r][i] += t;
+                    xs[r * D + lane + 64 * i] += t;
                 }
             return true;
         }
@@ -403,7 +408,7 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
 }
 
 template <int D, int R>
-__device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int lane) {
+__device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int lane) {
     constexpr int EPL = D / 64;
     unsigned* ctl = reinterpret_cast<unsigned*>(lds + ly.ctl);
     int* st = reinterpret_cast<int*>(lds + ly.st);
@@ -454,15 +459,11 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
     for (; s < a.nsteps && ok; ++s) {
         u64* sw = a.scratch + (size_t)s * a.step_words;
         const unsigned tag = (unsigned)s + 1u;
-        i64 xs[R][EPL];  // this CU's copy of the residual stream (int64 fixed point)
+        // this CU's copy of the residual stream (int64 fixed point), kept in LDS: as registers it
+        // pushed the kernel past 256 VGPRs at two rows (scratch spills in every phase)
+        i64* xs = reinterpret_cast<i64*>(lds + ly.xs);
         for (int l = 0; l < L && ok; ++l) {
             const Layer lw = a.layers[l];
-            if (s == a.fault_step && l == L - 1 && blockIdx.x == G - 1) {  // test hook: an aborted hand-off
-                set_err(a, E_INJECTED, 10 * l, s);
-                lds_st(ctl + C_ABORT, 1u);
-                ok = false;
-                break;
-            }
             stamp(a, s, l, 0, lane);
             if (l == 0) {
                 stamp_val(a, s, 0, 26, __builtin_amdgcn_s_memtime());
@@ -479,7 +480,7 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
 #pragma unroll
                     for (int i = 0; i < EPL; ++i) {
                         const int e = lane + 64 * i;
-                        xs[r][i] = f2fix(bf16_to_f32(a.wte[(size_t)tok[r] * D + e]) +
+                        xs[r * D + e] = f2fix(bf16_to_f32(a.wte[(size_t)tok[r] * D + e]) +
                                          bf16_to_f32(a.wpe[(size_t)pos[r] * D + e]));
                     }
             } else {
@@ -493,7 +494,7 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r][i]);
+                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
             stamp(a, s, l, 1, lane);
             layer_norm<D, R>(xf, gg, bb, a.eps, xn, lane);
             unsigned pid = pid_of(s, l, 0, L);
@@ -578,7 +579,7 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r][i]);
+                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
             layer_norm<D, R>(xf, gg, bb, a.eps, xn, lane);
             pid = pid_of(s, l, 2, L);
             lds_st(ctl + C_READY, pid);
@@ -598,6 +599,12 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
             }
         }
         if (!ok) break;
+        if (s == a.fault_step && blockIdx.x == G - 1) {  // test hook: an aborted hand-off (before the argmax)
+            set_err(a, E_INJECTED, 10 * L, s);
+            lds_st(ctl + C_ABORT, 1u);
+            ok = false;
+            break;
+        }
         // ---------------- ln_f + LM head + argmax
         {
             float xf[R][EPL];
@@ -610,7 +617,7 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r][i]);
+                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
             stamp(a, s, L, 0, lane);
             stamp_val(a, s, L, 26, __builtin_amdgcn_s_memtime());
             stamp_val(a, s, L, 27, wall_clock64());
@@ -718,7 +725,7 @@ __device__ void comm_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly,
 constexpr int LB = 8;  // units per batch (the ring is a multiple of LB KiB)
 constexpr unsigned BATCH = LB * 1024u;
 template <bool NT>
-__device__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int j, int lane) {
+__device__ __forceinline__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int j, int lane) {
     unsigned* ctl = reinterpret_cast<unsigned*>(lds + ly.ctl);
     const unsigned RB = (unsigned)a.ring_bytes;
     const unsigned SB = (unsigned)cu.step_bytes;
@@ -864,38 +871,42 @@ __device__ __forceinline__ f32x4_t mfma_rows16(const char* ring, unsigned gro, u
 // this wave's 16-row output tiles t = w, w + NC, ... (t < ntiles) of a K-major block [16 ntiles][KP]
 // at ring offset bro (bro < RB): out[m][o0 + 16 t + l] = sum_k A[m][k] * Blk[16 t + l][k]
 // (v_mfma_f32_16x16x16_bf16 per 16-deep k block; afr[kb]: this lane's A fragment, row l & 15,
-// k = 16 kb + 4 (l >> 4) .. + 4).  Every B fragment of the wave is read before the first MFMA;
-// results go to part[m][o0 + ..] (lanes < 16).  Offsets stay below 2 RB (a block is smaller than
-// the ring), so one conditional subtract wraps them -- no integer division per fragment.
+// k = 16 kb + 4 (l >> 4) .. + 4); results go to part[m][o0 + ..] (lanes < 16).  Tiles go TWO at a
+// time (their B fragments read before their MFMAs): a whole-block unroll kept up to D / 64 f32x4
+// accumulators live and pushed the kernel past 256 VGPRs into scratch (r4: 768-wide batch 1 went
+// from 30 to 51 ms).  Offsets stay below 2 RB (a block is smaller than the ring), so one
+// conditional subtract wraps them -- no integer division per fragment.
 template <int D, int R, int KB>
 __device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsigned RB, int KP, int nkb, int ntiles,
                                            int o0, const bf16x4_t (&afr)[KB], float* part, int w, int lane) {
-    constexpr int TPW = D / 16 / NC;  // the most tiles a wave may own (a block of all D outputs)
-    static_assert((D / 16) % NC == 0, "tiles per wave");
     const int n = lane & 15, kq = lane >> 4;
     const unsigned base = bro + (unsigned)((16 * w + n) * KP + 4 * kq) * 2u;
     const unsigned tstep = (unsigned)(16 * NC * KP) * 2u;
-    f32x4_t acc[TPW];
+    for (int j = 0; w + NC * j < ntiles; j += 2) {
+        const bool two = w + NC * (j + 1) < ntiles;
+        bf16x4_t b0[KB], b1[KB];
 #pragma unroll
-    for (int j = 0; j < TPW; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-        if (kb >= nkb) break;
-        bf16x4_t bv[TPW];
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-            if (w + NC * j < ntiles) bv[j] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * j + 32u * kb, RB));
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-            if (w + NC * j < ntiles) acc[j] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], bv[j], acc[j], 0, 0, 0);
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-            if (w + NC * j < ntiles) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) part[r * D + o0 + 16 * (w + NC * j) + lane] = acc[j][r];
+        for (int kb = 0; kb < KB; ++kb) {
+            if (kb < nkb) {
+                b0[kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * j + 32u * kb, RB));
+                if (two) b1[kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * (j + 1) + 32u * kb, RB));
             }
+        }
+        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            if (kb < nkb) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b0[kb], acc0, 0, 0, 0);
+                if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b1[kb], acc1, 0, 0, 0);
+            }
+        }
+        if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                part[r * D + o0 + 16 * (w + NC * j) + lane] = acc0[r];
+                if (two) part[r * D + o0 + 16 * (w + NC * (j + 1)) + lane] = acc1[r];
+            }
+        }
     }
 }
 
@@ -950,7 +961,7 @@ __device__ __forceinline__ void os_merge(OnlineS& z, float m2, float l2, const f
 }
 
 template <int D, int R, int PFG>
-__device__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int w, int lane) {
+__device__ __forceinline__ void compute_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int w, int lane) {
     constexpr int KBMAX = 4;  // k blocks of 16 per K-major block (K <= 64: a head, a slice)
     unsigned* ctl = reinterpret_cast<unsigned*>(lds + ly.ctl);
     const int* st = reinterpret_cast<const int*>(lds + ly.st);

@@ -115,6 +115,12 @@ for task in "$@"; do
             find $D -name "*_kernel_trace.csv" -delete
             for f in $(find $D -name "*kernel_stats.csv"); do python scripts/kstats.py "$f" > "${f%.csv}.summary.txt"; done
             grep '^{' $D/run.log; head -14 $(find $D -name "*kernel_stats.summary.txt" | head -1) ;;
+        dftrace:*)  # dftrace:<tag>:<batch>[:ENV=v,...]  in-kernel phase trace of the dataflow decode -> gpurun_out/dftrace_<tag>.json
+            spec=${task#dftrace:}; tag=${spec%%:*}; rest=${spec#*:}; b=${rest%%:*}; envs=""
+            [[ $rest == *:* ]] && envs=${rest#*:}
+            step 300 gpurun_out/dftrace_$tag.log env ${envs//,/ } python -u scripts/df_trace.py --model gpt2 --batch "$b" \
+                --out gpurun_out/dftrace_$tag.json
+            tail -2 gpurun_out/dftrace_$tag.log | cut -c1-300 ;;
         dfsweep:*)  # dfsweep:<df_sweep.sh args, ';' for spaces>  e.g. dfsweep:-b;1,2;default;DLMS_DF_J=1
             spec=${task#dfsweep:}
             step 900 gpurun_out/dfsweep.log bash scripts/df_sweep.sh -o gpurun_out/df_sweep.jsonl ${spec//;/ }
