@@ -99,8 +99,8 @@ class RelevanceGate:
         self._cached(text)
 
     # ------------------------------------------------------------------ query batching
-    def _score(self, text: str, a: torch.Tensor) -> float:
-        """Cosine(query embedding, ``a``), computed in the next shared batch."""
+    def _submit(self, text: str, a: torch.Tensor) -> Future:
+        """Queue the query for the next shared batch; the Future resolves to cosine(query, ``a``)."""
         fut: Future = Future()
         ids = self.tok.encode(text)
         with self._pcv:
@@ -109,7 +109,11 @@ class RelevanceGate:
                 self._batcher.start()
             self._pending.append((ids, a, fut))
             self._pcv.notify()
-        return fut.result()
+        return fut
+
+    def _score(self, text: str, a: torch.Tensor) -> float:
+        """Cosine(query embedding, ``a``), computed in the next shared batch."""
+        return self._submit(text, a).result()
 
     def _cosines(self, q: torch.Tensor, a: torch.Tensor) -> list[float]:
         if hasattr(self.encoder, "cosine"):  # HIP cosine kernel: [n, n], keep the diagonal
@@ -145,6 +149,21 @@ class RelevanceGate:
 
     def check(self, query: str, assignment_text: str) -> tuple[bool, float]:
         s = self.similarity(query, assignment_text)
+        return s >= self.threshold, s
+
+    async def check_async(self, query: str, assignment_text: str) -> tuple[bool, float]:
+        """``check`` for an event loop: the query waits for its shared batch WITHOUT holding a
+        thread (the LMS aio front end's GetLLMAnswer); only an assignment-embedding cache miss
+        (normally computed when the PostAssignment entry was applied) runs on the executor."""
+        import asyncio
+
+        loop = asyncio.get_running_loop()
+        k = self._key(assignment_text)
+        with self._lock:
+            a = self._cache.get(k)
+        if a is None:
+            a = await loop.run_in_executor(None, self._cached, assignment_text)
+        s = float(await asyncio.wrap_future(self._submit(query, a)))
         return s >= self.threshold, s
 
     def attach_state(self, state):

@@ -156,6 +156,9 @@ class TutoringClient:
             c.close()
 
 
+_SLOW = object()  # _llm_prelude_fast: "run the full prelude on the worker pool"
+
+
 class LMSServicer:
     def __init__(self, node, state, addresses: dict[int, str], tutor: TutoringClient | None = None, gate=None,
                  write_timeout: float = 5.0, forward_timeout: float = 130.0, replicator=None):
@@ -455,6 +458,43 @@ class LMSServicer:
             return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
         return None
 
+    def _llm_prelude_fast(self, request):
+        """The common case of ``_llm_prelude`` without blocking the event loop: a student session
+        present on this node (a leader only once its read fence is already satisfied) with an
+        assignment.  Returns ``_SLOW`` when the full prelude must run on the pool (unknown token
+        or no assignment here -- possibly a forward to the leader --, an unfenced leader, a gate
+        without ``check_async``), the assignment text when the gate is to decide, else the final
+        response or None (no gate: straight to the tutoring tier)."""
+        if self.gate is not None and not hasattr(self.gate, "check_async"):
+            return _SLOW
+        if self.node.is_leader and not self.node.read_ready():
+            return _SLOW
+        s = self.state.session(request.token)
+        if s is None:
+            return _SLOW
+        if s["role"] != "student":
+            return pb.QueryResponse(success=True, response=MSG_LLM_ONLY_STUDENTS)
+        user = s["username"]
+        text = self.state.read(lambda d: d["assignments"][user][0]["text"] if d["assignments"].get(user) else None)
+        if text is None:
+            return _SLOW
+        if self.gate is not None:
+            return text
+        return None if self.tutor is not None else pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+
+    async def _gate_async(self, request, assignment_text: str):
+        tg = time.perf_counter()
+        relevant, sim = await self.gate.check_async(request.query, assignment_text)
+        METRICS.observe("gate_ms", (time.perf_counter() - tg) * 1e3)
+        TRACER.complete("lms.gate", tg, cat="lms", similarity=round(float(sim), 4), relevant=bool(relevant))
+        METRICS.observe("gate_similarity", sim)
+        if not relevant:
+            METRICS.inc("gate_rejected_total")
+            return pb.QueryResponse(success=True, response=MSG_LLM_IRRELEVANT)
+        if self.tutor is None:
+            return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+        return None
+
     def _llm_done(self, t0: float, tt: float):
         TRACER.complete("lms.tutor_call", tt, cat="lms")
         TRACER.complete("lms.GetLLMAnswer", t0, cat="lms")
@@ -475,14 +515,22 @@ class LMSServicer:
         return resp
 
     async def GetLLMAnswerAsync(self, request, context):
-        """GetLLMAnswer for the ``grpc.aio`` front end (LMSServer ``frontend="aio"``): the short
-        prelude (state reads, the batched relevance gate) runs on the server's thread pool, the
-        long tutoring call is awaited on the event loop -- a query in flight holds no thread, so
-        one LMS node carries thousands of concurrent tutoring queries."""
+        """GetLLMAnswer for the ``grpc.aio`` front end (LMSServer ``frontend="aio"``): the session
+        and assignment reads run on the event loop (a lock-protected dict lookup each), the
+        batched relevance gate and the long tutoring call are awaited -- a query in flight holds
+        no thread at all, so one LMS node carries thousands of concurrent tutoring queries and the
+        worker pool stays free for the Raft RPCs.  Only the rare slow cases (a follower's forward
+        to the leader, a fenced read that has to wait) go to the pool, through ``_llm_prelude``."""
         import asyncio
 
         t0 = time.perf_counter()
-        early = await asyncio.get_running_loop().run_in_executor(None, self._llm_prelude, request, context)
+        fast = self._llm_prelude_fast(request)
+        if fast is _SLOW:
+            early = await asyncio.get_running_loop().run_in_executor(None, self._llm_prelude, request, context)
+        elif isinstance(fast, str):  # the assignment text: the gate decides
+            early = await self._gate_async(request, fast)
+        else:
+            early = fast
         if early is not None:
             return early
         tt = time.perf_counter()

@@ -216,6 +216,17 @@ class RaftNode:
                 self._applied_cv.wait(rem)
         return True
 
+    def read_ready(self) -> bool:
+        """Non-blocking ``read_barrier``: True when this node leads and has already applied
+        everything committed up to the first entry of its own term (local reads are fenced)."""
+        with self._lock:
+            if self.core.role != LEADER:
+                return False
+            target = self.core.commit_index
+            if self.core.storage.term_at(target) != self.core.current_term:
+                return False
+        return self.applied_index >= target
+
     def read_barrier(self, timeout: float = 5.0) -> bool:
         """Leader-side read fence: wait until this leader has applied everything committed up to
         the first entry of its own term (so local reads reflect every acknowledged write)."""

@@ -45,14 +45,26 @@ def start_tutor(servicer=None):
     return srv, port, servicer
 
 
-class KeywordGate:
-    """Deterministic gate for service tests: relevant iff the query shares a word with the text."""
+class SyncKeywordGate:
+    """Deterministic gate for service tests: relevant iff the query shares a word with the text.
+    (No ``check_async``: GetLLMAnswer runs the worker-pool prelude.)"""
 
     def check(self, query: str, text: str):
         q = set(query.lower().split())
         t = set(text.lower().split())
         sim = len(q & t) / max(1, len(q))
         return sim > 0, sim
+
+
+class KeywordGate(SyncKeywordGate):
+    """The same gate with the aio front end's thread-free path (service.py ``_llm_prelude_fast``)."""
+
+    def __init__(self):
+        self.async_calls = 0
+
+    async def check_async(self, query: str, text: str):
+        self.async_calls += 1
+        return self.check(query, text)
 
 
 class Cluster:

@@ -92,6 +92,7 @@ def test_full_workflow_exact_strings(cluster):
     assert st.GetLLMAnswer(pb.QueryRequest(token=tb, query="x"), timeout=30).response == S.MSG_LLM_ONLY_STUDENTS
     assert st.GetLLMAnswer(pb.QueryRequest(token="bad", query="x"), timeout=30).response == S.MSG_LLM_INVALID_SESSION
     assert cluster.tutor.calls == ["explain leader election"]
+    assert cluster.gate.async_calls == 2  # the relevant + irrelevant queries took the thread-free path
 
     assert st.Logout(pb.LogoutRequest(token=ta), timeout=10).success
     assert not st.Logout(pb.LogoutRequest(token=ta), timeout=10).success
@@ -140,3 +141,31 @@ def test_leader_failover_keeps_data_and_sessions(cluster):
     assert st2.GetGrade(pb.GetGradeRequest(token=tok), timeout=10).grade == S.MSG_NO_ASSIGNMENTS
     d = cluster.servers[new].state.view()
     assert [q["query"] for q in d["queries"]["erin"]] == ["q1", "q2"]
+
+
+def test_llm_path_with_a_sync_only_gate(tmp_path):
+    """A gate without ``check_async`` (any synchronous relevance check): GetLLMAnswer runs its
+    prelude on the worker pool and gives the same answers as the thread-free path."""
+    from lms_harness import SyncKeywordGate
+
+    tsrv, tport, tutor = start_tutor()
+    c = Cluster(3, tmp_path, tutor_address=f"127.0.0.1:{tport}", gate=SyncKeywordGate())
+    try:
+        lid = c.wait_leader()
+        from distributed_lms_raft_llm_amd import wire
+        import grpc
+
+        with grpc.insecure_channel(c.addrs[lid]) as ch:
+            st = wire.Stub("LMS", ch)
+            assert st.Register(pb.RegisterRequest(username="s", password="pw", role="student"), timeout=10).success
+            tok = login(st, "s")
+            assert st.Post(pb.PostRequest(token=tok, type="assignment", file=make_pdf("raft leader election terms"),
+                                          filename="a.pdf"), timeout=30).success
+            r = st.GetLLMAnswer(pb.QueryRequest(token=tok, query="explain leader election"), timeout=30)
+            assert r.success and r.response.startswith("Question: explain leader election")
+            r = st.GetLLMAnswer(pb.QueryRequest(token=tok, query="best pizza toppings"), timeout=30)
+            assert r.response == S.MSG_LLM_IRRELEVANT
+        assert tutor.calls == ["explain leader election"]
+    finally:
+        c.close()
+        tsrv.stop(0)
