@@ -362,38 +362,36 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    // phase 2: the whole buffer (almost always complete by now)
+    // phase 2: the whole buffer (almost always complete by now), one (row, copy) slab of EPL words
+    // at a time: a slab whose words all carry their final count is final for good (the buffer is
+    // fresh per step), so it is added to xs at once and never read again -- only EPL words are
+    // live per pass (all COPIES x R x EPL of them at once pushed the 2-row kernel into scratch)
+    unsigned pending = (1u << (COPIES * R)) - 1u;
     for (;;) {
-        u64 v[COPIES][R][EPL];
 #pragma unroll
         for (int c = 0; c < COPIES; ++c)
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+            for (int r = 0; r < R; ++r) {
+                if (!(pending & (1u << (c * R + r)))) continue;
+                u64 v[EPL];
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) {
                     const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (((c * R + r) * D) + lane + 64 * i) * 8, 0,
                                                                         16 /* sc1 */);
-                    v[c][r][i] = ((u64)x[1] << 32) | x[0];
+                    v[i] = ((u64)x[1] << 32) | x[0];
                 }
-        bool ok = true;
+                bool ok = true;
 #pragma unroll
-        for (int c = 0; c < COPIES; ++c)
+                for (int i = 0; i < EPL; ++i) ok &= (int)(v[i] >> 56) == ec[c];
+                if (__all(ok)) {
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int i = 0; i < EPL; ++i) ok &= (int)(v[c][r][i] >> 56) == ec[c];
-        if (__all(ok)) {
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int i = 0; i < EPL; ++i) {
-                    i64 t = f2fix(bias[i]);
-#pragma unroll
-                    for (int c = 0; c < COPIES; ++c) t += (i64)(v[c][r][i] & CNT_MASK) - (i64)ec[c] * CNT_BIAS;
-                    xs[r * D + lane + 64 * i] += t;
+                    for (int i = 0; i < EPL; ++i)
+                        xs[r * D + lane + 64 * i] += (i64)(v[i] & CNT_MASK) - (i64)ec[c] * CNT_BIAS +
+                                                     (c == 0 ? f2fix(bias[i]) : 0);
+                    pending &= ~(1u << (c * R + r));
                 }
-            return true;
-        }
+            }
+        if (!pending) return true;
         if ((unsigned)__builtin_amdgcn_readfirstlane((int)gld32(a.err)) || lds_ld(ctl + C_ABORT)) {
             lds_st(ctl + C_ABORT, 1u);
             return false;

@@ -1,8 +1,9 @@
 """One-shot xGMI collectives (ops/csrc/xgmi.hip, parallel/xgmi.py) on ONE GPU: two processes share
 cuda:0 and map each other's buffers through hipIpc handles exactly as TP ranks on different GPUs
 do (the cross-GPU xGMI run is the driver's 8-GPU node).  Checked against a plain fp32 sum in rank
-order (bit-exact), across message sizes that change the grid between calls (the slab-parity
-protocol), replayed from a hipGraph, and end to end in the TP engine."""
+order (bit-exact), the int64 integer all-reduce against an exact integer sum, across message sizes
+that change the grid between calls (the slab-parity protocol), replayed from a hipGraph, and end
+to end in the TP engine."""
 import os
 import socket
 
@@ -43,6 +44,12 @@ def _worker(rank, world, port, q):
             t = _data(rank, n, call).cuda()
             comm.all_reduce_(t)
             results[("ar", call)] = t.cpu().numpy()
+        # integer all-reduce (the TP fused layer's int64 fixed-point residual), eager
+        for call, n in enumerate((2, 2 * 1280, 2 * 3 * 1600, 64 * 1024)):
+            g = torch.Generator().manual_seed(500 * rank + call)
+            t = torch.randint(-(1 << 46), 1 << 46, (n,), generator=g, dtype=torch.int64).cuda()
+            comm.all_reduce_i64_(t)
+            results[("i64", call)] = t.cpu().numpy()
         keys = torch.arange(37, dtype=torch.int64) * 1000 + rank
         out = torch.zeros(world, 37, dtype=torch.int64, device="cuda")
         comm.all_gather_u64(keys.cuda(), out)
@@ -97,6 +104,11 @@ def test_xgmi_allreduce_allgather_two_processes():
         want = _data(0, n, call) + _data(1, n, call)  # rank order, fp32: bit-exact
         for r in (0, 1):
             assert torch.equal(torch.from_numpy(res[r][("ar", call)]), want), (call, n, r)
+    for call, n in enumerate((2, 2 * 1280, 2 * 3 * 1600, 64 * 1024)):
+        parts = [torch.randint(-(1 << 46), 1 << 46, (n,), generator=torch.Generator().manual_seed(500 * p + call),
+                               dtype=torch.int64) for p in (0, 1)]
+        for r in (0, 1):
+            assert torch.equal(torch.from_numpy(res[r][("i64", call)]), parts[0] + parts[1]), (call, n, r)
     want_ag = torch.stack([torch.arange(37) * 1000 + p for p in (0, 1)])
     assert all(torch.equal(torch.from_numpy(res[r]["ag"]), want_ag) for r in (0, 1))
     for rep in range(5):
