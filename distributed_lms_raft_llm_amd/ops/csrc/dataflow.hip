@@ -27,7 +27,8 @@
 //   E1  residual complete (previous MLP's atomics + counter, or the embedding) -> every CU: LN1,
 //       its rows of W_qkv (dot) -> q/k/v as tagged 8-byte granules (+ K/V cache rows)
 //   E2  per-head granules -> the attention CUs of that head: attention over the cache, then W_o
-//       for the CU's slice of OUTPUT columns (all 64 head dims) -> counted fixed-point atomics into XA
+//       for the CU's slice of head dims (or, opt-in, of output columns) -> counted fixed-point
+//       atomics into XA
 //   E3  XA complete (every word's contribution count) -> every CU: x += XA + b_o, LN2, the c_fc
 //       rows of its intermediate slice (h = bf16(gelu(.))), c_proj for its slice of output columns
 //       -> counted fixed-point atomics into XM
@@ -86,7 +87,8 @@ struct Cu {           // per-CU assignment (host-built table, ops/dataflow.py as
     int f0, nf;       // intermediate (c_fc row) slice [f0, f0 + nf)
     int v0, nv;       // LM-head (wte) rows [v0, v0 + nv)
     int ah;           // attention head (-1: none)
-    int ao0, aon;     // its W_o output columns [ao0, ao0 + aon) (all 64 head dims)
+    int ao0, aon;     // its W_o output columns [ao0, ao0 + aon) ...
+    int ak0, akn;     // ... over the head dims [ak0, ak0 + akn)
     int pd0, pdn;     // c_proj output columns [pd0, pd0 + pdn) of the slice
     int acp, mcp;     // residual copy of the attention / MLP contributions
     int pad;
@@ -869,41 +871,41 @@ __device__ __forceinline__ f32x4_t mfma_rows16(const char* ring, unsigned gro, u
 // this wave's 16-row output tiles t = w, w + NC, ... (t < ntiles) of a K-major block [16 ntiles][KP]
 // at ring offset bro (bro < RB): out[m][o0 + 16 t + l] = sum_k A[m][k] * Blk[16 t + l][k]
 // (v_mfma_f32_16x16x16_bf16 per 16-deep k block; afr[kb]: this lane's A fragment, row l & 15,
-// k = 16 kb + 4 (l >> 4) .. + 4); results go to part[m][o0 + ..] (lanes < 16).  Tiles go TWO at a
-// time (their B fragments read before their MFMAs): a whole-block unroll kept up to D / 64 f32x4
-// accumulators live and pushed the kernel past 256 VGPRs into scratch (r4: 768-wide batch 1 went
-// from 30 to 51 ms).  Offsets stay below 2 RB (a block is smaller than the ring), so one
-// conditional subtract wraps them -- no integer division per fragment.
-template <int D, int R, int KB>
+// k = 16 kb + 4 (l >> 4) .. + 4); results go to part[m][o0 + ..] (lanes < 16).  Tiles go U at a
+// time (U = 3), all their B fragments read before their MFMAs: a whole-block unroll kept up to D / 64 f32x4
+// accumulators live and pushed the kernel past 256 VGPRs into scratch (r4: 768-wide batch 1 from
+// 30 to 51 ms; U = 4 spills too), fewer left the LDS latency exposed.  Offsets stay below 2 RB (a
+// block is smaller than the ring), so one conditional subtract wraps them -- no integer division.
+template <int D, int R, int KB, int U = 3>
 __device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsigned RB, int KP, int nkb, int ntiles,
                                            int o0, const bf16x4_t (&afr)[KB], float* part, int w, int lane) {
     const int n = lane & 15, kq = lane >> 4;
     const unsigned base = bro + (unsigned)((16 * w + n) * KP + 4 * kq) * 2u;
     const unsigned tstep = (unsigned)(16 * NC * KP) * 2u;
-    for (int j = 0; w + NC * j < ntiles; j += 2) {
-        const bool two = w + NC * (j + 1) < ntiles;
-        bf16x4_t b0[KB], b1[KB];
+    for (int j = 0; w + NC * j < ntiles; j += U) {
+        bf16x4_t b[U][KB];
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            if (kb < nkb) {
-                b0[kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * j + 32u * kb, RB));
-                if (two) b1[kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * (j + 1) + 32u * kb, RB));
-            }
-        }
-        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            if (kb < nkb) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b0[kb], acc0, 0, 0, 0);
-                if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b1[kb], acc1, 0, 0, 0);
-            }
-        }
+            for (int kb = 0; kb < KB; ++kb)
+                if (kb < nkb && w + NC * (j + u) < ntiles)
+                    b[u][kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * (j + u) + 32u * kb, RB));
+        f32x4_t acc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (kb < nkb && w + NC * (j + u) < ntiles)
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b[u][kb], acc[u], 0, 0, 0);
         if (lane < 16) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                part[r * D + o0 + 16 * (w + NC * j) + lane] = acc0[r];
-                if (two) part[r * D + o0 + 16 * (w + NC * (j + 1)) + lane] = acc1[r];
-            }
+            for (int u = 0; u < U; ++u)
+                if (w + NC * (j + u) < ntiles) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) part[r * D + o0 + 16 * (w + NC * (j + u)) + lane] = acc[u][r];
+                }
         }
     }
 }
@@ -1168,7 +1170,7 @@ __device__ __forceinline__ void compute_wave(const Args& a, const Cu& cu, char* 
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 bf16x4_t afr[KBMAX];
                 const int nkb = KO / 16;
-                load_afr<KBMAX, R>(hb, 0, 64, nkb, afr, lane);  // all 64 head dims
+                load_afr<KBMAX, R>(hb, cu.ak0, cu.akn, nkb, afr, lane);  // this CU's head dims
                 if (!wait_loaded_t(ctl, fbase, a, s, &ringwait, tracing)) return;  // the whole W_o block
                 asm volatile("" ::: "memory");
                 mfma_block<D, R, KBMAX>(ring, obase % RB, RB, KO, nkb, aon / 16, ao0, afr, part, w, lane);

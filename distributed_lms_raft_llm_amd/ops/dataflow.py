@@ -31,8 +31,8 @@ P = ctypes.c_void_p
 
 
 class DfCu(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_int) for n in ("q0", "nq", "f0", "nf", "v0", "nv", "ah", "ao0", "aon", "pd0", "pdn", "acp",
-                                            "mcp", "pad")] + \
+    _fields_ = [(n, ctypes.c_int) for n in ("q0", "nq", "f0", "nf", "v0", "nv", "ah", "ao0", "aon", "ak0", "akn",
+                                            "pd0", "pdn", "acp", "mcp", "pad")] + \
                [("off", ctypes.c_longlong), ("step_bytes", ctypes.c_longlong)]
 
 
@@ -110,13 +110,16 @@ class CuPlan:
     pdn: int = 0
     mcp: int = 0      # residual copy its MLP contributions go to
     ah: int = -1      # attention head (-1: none) ...
-    ao0: int = 0      # ... and its W_o output columns [ao0, ao0 + aon) (all 64 head dims)
+    ao0: int = 0      # ... its W_o output columns [ao0, ao0 + aon) ...
     aon: int = 0
+    ak0: int = 0      # ... over the head dims [ak0, ak0 + akn)
+    akn: int = 0
     acp: int = 0      # residual copy its attention contributions go to
 
     def layer_elems(self, d: int, ko: int, kf: int) -> int:
         """bf16 elements of one layer in the stream: W_qkv rows (padded), the K-major W_o block
-        [aon][ko] (attention CUs), the c_fc rows (padded), the K-major c_proj block [pdn][kf]."""
+        [aon][ko] (attention CUs: its output columns x its head dims), the c_fc rows (padded),
+        the K-major c_proj block [pdn][kf]."""
         return (self.nq + self.nf) * (d + ROW_PAD) + (self.aon * ko if self.ah >= 0 else 0) + self.pdn * kf
 
     def step_elems(self, L: int, d: int, ko: int, kf: int) -> int:
@@ -124,13 +127,12 @@ class CuPlan:
 
 
 def block_k(cus: list[CuPlan]) -> tuple[int, int]:
-    """(ko, kf): K of the W_o / c_proj blocks, padded to the 16-deep MFMA step (same for all CUs):
-    a W_o block holds all 64 dims of its head."""
-    return 64, pad16(max(cu.nf for cu in cus))
+    """(ko, kf): K of the W_o / c_proj blocks, padded to the 16-deep MFMA step (same for all CUs)."""
+    return pad16(max((cu.akn for cu in cus), default=16)), pad16(max(cu.nf for cu in cus))
 
 
 def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int, J: int = 1,
-           copies: int = 2) -> list[CuPlan]:
+           copies: int = 2, attn_split: str = "dims") -> list[CuPlan]:
     """Work of each of G CUs (see module docstring).
 
     * W_qkv rows and LM-head rows: split evenly over the G CUs.
@@ -139,13 +141,16 @@ def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int
       CU adds d / J residual words per row instead of d (the per-CU atomic issue and the memory-side
       atomic count of the post-MLP edge shrink J-fold; the extra c_fc rows are prefetched weight
       bytes, off the critical path).  Slice i's contributions go to residual copy i % copies.
-    * Attention: each head on GS CUs; each computes the whole head and publishes its W_o output
-      columns [g d/GS, (g + 1) d/GS) (d / GS words instead of d), into copy h % copies.
-      Attention CU a = h * GS + g sits at CU (a * G) // A, spreading them over all XCDs.
-    Every residual word then receives exactly I contributions after the MLP (n_head after the
-    attention), split over the copies the same way for every word."""
-    if n_head * GS > G or d % (16 * GS):
-        raise ValueError(f"dataflow: GS={GS}: need n_head * GS <= {G} and d % (16 GS) == 0")
+    * Attention: each head on GS CUs, each computing the whole head.  ``attn_split="dims"`` (the
+      default): CU g owns head dims [g 64/GS, (g + 1) 64/GS) of W_o and publishes all d outputs
+      (contribution copy a % copies); ``"outputs"``: it owns all 64 dims and publishes the output
+      columns [g d/GS, (g + 1) d/GS) (copy h % copies) -- fewer atomics per CU, but measured
+      slower at GPT-2 widths (its W_o phase is longer, the edges did not shorten:
+      profiles/r4_df_partition_sweep.jsonl).  Attention CU a = h * GS + g sits at CU (a * G) // A,
+      spreading them over all XCDs.
+    Every residual word then receives the same number of contributions per copy."""
+    if n_head * GS > G or 64 % GS or (attn_split == "outputs" and d % (16 * GS)):
+        raise ValueError(f"dataflow: GS={GS} does not split heads over {G} CUs")
     if G % J or d % (16 * J):
         raise ValueError(f"dataflow: J={J} must divide G={G} and d / J must be a multiple of 16")
     I = G // J
@@ -162,7 +167,11 @@ def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int
     for a in range(A):
         cu = cus[(a * G) // A]
         h, g = divmod(a, GS)
-        cu.ah, cu.ao0, cu.aon, cu.acp = h, g * (d // GS), d // GS, h % copies
+        cu.ah = h
+        if attn_split == "outputs":
+            cu.ao0, cu.aon, cu.ak0, cu.akn, cu.acp = g * (d // GS), d // GS, 0, 64, h % copies
+        else:
+            cu.ao0, cu.aon, cu.ak0, cu.akn, cu.acp = 0, d, g * (64 // GS), 64 // GS, a % copies
     return cus
 
 
@@ -195,8 +204,11 @@ def pack_weights(w, cus: list[CuPlan], device) -> tuple[torch.Tensor, list[int]]
         for c, cu in enumerate(cus):
             o = starts[c] + l * cu.layer_elems(d, ko, kf)
             pieces = [qkv[cu.q0: cu.q0 + cu.nq].reshape(-1)]
-            if cu.ah >= 0:  # W_o[out, in]: outputs [ao0, +aon) x the head's 64 input dims
-                pieces.append(lw.w_o[cu.ao0: cu.ao0 + cu.aon, cu.ah * 64: cu.ah * 64 + 64].reshape(-1))
+            if cu.ah >= 0:  # W_o[out, in]: outputs [ao0, +aon) x the head dims [ak0, +akn), K padded to ko
+                blk = torch.zeros(cu.aon, ko, dtype=torch.bfloat16, device=device)
+                k0 = cu.ah * 64 + cu.ak0
+                blk[:, : cu.akn] = lw.w_o[cu.ao0: cu.ao0 + cu.aon, k0: k0 + cu.akn]
+                pieces.append(blk.reshape(-1))
             pieces.append(fc[cu.f0: cu.f0 + cu.nf].reshape(-1))
             blk = torch.zeros(cu.pdn, kf, dtype=torch.bfloat16, device=device)
             blk[:, : cu.nf] = lw.w_p[cu.pd0: cu.pd0 + cu.pdn, cu.f0: cu.f0 + cu.nf]
@@ -249,15 +261,17 @@ class DataflowDecoder:
         cus = int(props.multi_processor_count)
         G = grid or int(os.environ.get("DLMS_DF_GRID", "0")) or min(cus * 25 // 32, 256)
         gs = gs or int(os.environ.get("DLMS_DF_GS", "2"))
-        while (cfg.n_head * gs > G or cfg.n_embd % (16 * gs)) and gs > 1:
+        split = os.environ.get("DLMS_DF_ATTN_SPLIT", "dims")
+        while (cfg.n_head * gs > G or 64 % gs or (split == "outputs" and cfg.n_embd % (16 * gs))) and gs > 1:
             gs //= 2
-        # MLP output groups J (see assign): as many as keep a slice's c_fc rows <= 64 and the
-        # largest stream piece inside the ring -- 4 at d 768, 2 at 1024, 1 for large / XL
-        j = j or int(os.environ.get("DLMS_DF_J", "0")) or {768: 4, 1024: 2}.get(cfg.n_embd, 1)
+        # MLP output groups J (see assign): 1 by default -- J = 2 / 4 (each CU publishing d / J
+        # residual words) measured slower at every width: the edges did not shorten and the
+        # duplicated c_fc rows lengthened the MLP phase (profiles/r4_df_partition_sweep.jsonl)
+        j = j or int(os.environ.get("DLMS_DF_J", "1"))
         while j > 1 and (G % j or -(-eng.w.ffn_local * j // G) > 64 or cfg.n_embd % (16 * j)):
             j -= 1
         self.G, self.GS, self.J = G, gs, j
-        self.cus = assign(cfg.n_embd, cfg.n_head, eng.w.ffn_local, cfg.vocab_padded, G, gs, j, self.COPIES)
+        self.cus = assign(cfg.n_embd, cfg.n_head, eng.w.ffn_local, cfg.vocab_padded, G, gs, j, self.COPIES, split)
         self.A = cfg.n_head * gs
         self.ko, self.kf = block_k(self.cus)
         if self.ko > 64 or self.kf > 64:
@@ -271,8 +285,9 @@ class DataflowDecoder:
         self.swl = -(-max_nv // 64) * 2 + 2
         tab = (DfCu * G)()
         for c, cu in enumerate(self.cus):
-            tab[c] = DfCu(cu.q0, cu.nq, cu.f0, cu.nf, cu.v0, cu.nv, cu.ah, cu.ao0, cu.aon, cu.pd0, cu.pdn, cu.acp,
-                          cu.mcp, 0, starts[c] * 2, cu.step_elems(cfg.n_layer, D, self.ko, self.kf) * 2)
+            tab[c] = DfCu(cu.q0, cu.nq, cu.f0, cu.nf, cu.v0, cu.nv, cu.ah, cu.ao0, cu.aon, cu.ak0, cu.akn, cu.pd0,
+                          cu.pdn, cu.acp, cu.mcp, 0, starts[c] * 2,
+                          cu.step_elems(cfg.n_layer, D, self.ko, self.kf) * 2)
         self.max_step_bytes = max(cu.step_elems(cfg.n_layer, D, self.ko, self.kf) for cu in self.cus) * 2
         self.cu_tab = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
         lt = (DfLayer * cfg.n_layer)()

@@ -9,10 +9,11 @@ from distributed_lms_raft_llm_amd.models.config import GPT2Config, gpt2_config
 from distributed_lms_raft_llm_amd.ops.dataflow import ROW_PAD, assign, block_k, pack_weights
 
 
+@pytest.mark.parametrize("split", ["dims", "outputs"])
 @pytest.mark.parametrize("name,G,GS,J", [("gpt2", 256, 4, 1), ("gpt2", 200, 2, 4), ("gpt2-medium", 200, 2, 2),
                                          ("gpt2-xl", 256, 4, 1), ("gpt2-xl", 200, 2, 1), ("gpt2-large", 200, 2, 1),
                                          ("gpt2-tiny", 64, 4, 2), ("gpt2", 80, 2, 1)])
-def test_assignment_covers_every_row_once(name, G, GS, J):
+def test_assignment_covers_every_row_once(name, G, GS, J, split):
     """Every W_qkv row and LM-head row on exactly one CU; every (intermediate column, output column)
     pair of c_proj on exactly one CU (the J CUs of a slice split its outputs); every (head, output
     column) of W_o on exactly one attention CU; and the per-copy contribution counts the kernel
@@ -22,7 +23,7 @@ def test_assignment_covers_every_row_once(name, G, GS, J):
     cfg = gpt2_config(name)
     d, H, F, V = cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded
     C = 2
-    cus = assign(d, H, F, V, G, GS, J, C)
+    cus = assign(d, H, F, V, G, GS, J, C, split)
     assert len(cus) == G
     for key, n in (("q", 3 * d), ("v", V)):
         covered = np.zeros(n, dtype=int)
@@ -36,18 +37,18 @@ def test_assignment_covers_every_row_once(name, G, GS, J):
         cp[cu.f0: cu.f0 + cu.nf, cu.pd0: cu.pd0 + cu.pdn] += 1
         per_word[cu.mcp, cu.pd0: cu.pd0 + cu.pdn] += 1
     assert (cp == 1).all()
-    cov = np.zeros((H, d), dtype=int)
+    cov = np.zeros((H, 64, d), dtype=int)  # (head, head dim, output column) of W_o
     att_word = np.zeros((C, d), dtype=int)
     att = [cu for cu in cus if cu.ah >= 0]
     assert len(att) == H * GS
     for cu in att:
-        cov[cu.ah, cu.ao0: cu.ao0 + cu.aon] += 1
+        cov[cu.ah, cu.ak0: cu.ak0 + cu.akn, cu.ao0: cu.ao0 + cu.aon] += 1
         att_word[cu.acp, cu.ao0: cu.ao0 + cu.aon] += 1
     assert (cov == 1).all()
     exp_att, exp_mlp = expected_contributions(cus, C)
     for c in range(C):
         assert (att_word[c] == exp_att[c]).all() and (per_word[c] == exp_mlp[c]).all()
-    assert sum(exp_att) == H and sum(exp_mlp) == G // J
+    assert sum(exp_att) == (H if split == "outputs" else H * GS) and sum(exp_mlp) == G // J
     assert max(cu.nq for cu in cus) <= 64 and max(cu.nf for cu in cus) <= 64
 
 
@@ -55,7 +56,7 @@ def test_assignment_rejects_bad_split():
     with pytest.raises(ValueError):
         assign(768, 12, 3072, 50304, 16, 4)  # 48 attention CUs on 16
     with pytest.raises(ValueError):
-        assign(768, 12, 3072, 50304, 256, 5)  # 768 / 5 output columns: not a multiple of 16
+        assign(768, 12, 3072, 50304, 256, 5)  # 5 does not split a head's 64 dims
     with pytest.raises(ValueError):
         assign(768, 12, 3072, 50304, 200, 2, 3)  # J must divide G
 
@@ -67,7 +68,7 @@ def test_packed_stream_matches_sources():
     cfg = GPT2Config("df-test", n_layer=2, n_embd=128, n_head=2, n_positions=64, vocab_size=300, eos_token_id=299)
     w = prepare_gpt2_weights(cfg, init_gpt2_weights(cfg, seed=3), "cpu")
     G, GS, J = 16, 4, 2
-    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, GS, J)
+    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, G, GS, J)  # (dims split: ko 16)
     packed, starts = pack_weights(w, cus, "cpu")
     ko, kf = block_k(cus)
     d, L = cfg.n_embd, cfg.n_layer
@@ -85,8 +86,10 @@ def test_packed_stream_matches_sources():
             assert torch.equal(rows(o, cu.nq), lw.w_qkv[cu.q0: cu.q0 + cu.nq])
             o += cu.nq * (d + ROW_PAD)
             if cu.ah >= 0:
-                blk = packed[o: o + cu.aon * ko].reshape(cu.aon, ko)  # K-major: [outputs][64 head dims]
-                assert torch.equal(blk, lw.w_o[cu.ao0: cu.ao0 + cu.aon, cu.ah * 64: cu.ah * 64 + 64])
+                blk = packed[o: o + cu.aon * ko].reshape(cu.aon, ko)  # K-major: [outputs][head dims]
+                k0 = cu.ah * 64 + cu.ak0
+                assert torch.equal(blk[:, : cu.akn], lw.w_o[cu.ao0: cu.ao0 + cu.aon, k0: k0 + cu.akn])
+                assert not blk[:, cu.akn:].any()
                 o += cu.aon * ko
             assert torch.equal(rows(o, cu.nf), lw.w_fc[cu.f0: cu.f0 + cu.nf])
             o += cu.nf * (d + ROW_PAD)
@@ -123,8 +126,9 @@ def _emulate_step(cfg, w, cus, tok, pos, kv):
             K = torch.cat([f(kv[l][0][hh]), qkv[d + hh * 64: d + (hh + 1) * 64][None]])
             V = torch.cat([f(kv[l][1][hh]), qkv[2 * d + hh * 64: 2 * d + (hh + 1) * 64][None]])
             p = torch.softmax(K @ q / 8.0, dim=0)
-            o = p @ V  # the whole head; this CU adds W_o for its output columns only
-            xa[cu.ao0: cu.ao0 + cu.aon] += f(lw.w_o[cu.ao0: cu.ao0 + cu.aon, hh * 64:(hh + 1) * 64]) @ o
+            o = p @ V  # the whole head; this CU adds W_o for its output columns x head dims only
+            k0 = hh * 64 + cu.ak0
+            xa[cu.ao0: cu.ao0 + cu.aon] += f(lw.w_o[cu.ao0: cu.ao0 + cu.aon, k0: k0 + cu.akn]) @ o[cu.ak0: cu.ak0 + cu.akn]
         h2 = ln(xa, lw.ln2_g, lw.ln2_b)
         xm = xa + f(lw.b_p)
         for cu in cus:
@@ -137,7 +141,8 @@ def _emulate_step(cfg, w, cus, tok, pos, kv):
     return ln(x, w.lnf_g, w.lnf_b)
 
 
-def test_split_reproduces_the_reference_step():
+@pytest.mark.parametrize("split,J", [("dims", 1), ("dims", 2), ("outputs", 2)])
+def test_split_reproduces_the_reference_step(split, J):
     """The per-CU decomposition (QKV rows, head-dim slices of W_o, c_fc/c_proj pairs, base adds)
     sums to exactly the reference forward (float64, no rounding)."""
     from distributed_lms_raft_llm_amd.engine.weights import prepare_gpt2_weights
@@ -147,7 +152,7 @@ def test_split_reproduces_the_reference_step():
     raw = init_gpt2_weights(cfg, seed=5)
     perturb_norms_and_biases(raw)
     w = prepare_gpt2_weights(cfg, raw, "cpu", dtype=torch.float32)
-    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, 8, 2, 2)
+    cus = assign(cfg.n_embd, cfg.n_head, cfg.n_inner, cfg.vocab_padded, 8, 2, J, 2, split)
     ref = GPT2Reference(cfg, raw, device="cpu", dtype=torch.float64)
     seq = [5, 17, 42, 7]
     cache = KVCache.allocate(cfg, 1, 8, dtype=torch.float64, device="cpu")
