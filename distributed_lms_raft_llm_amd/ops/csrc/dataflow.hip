@@ -126,6 +126,8 @@ struct Args {
     int ko, kf;  // K (padded to 16) of the per-CU W_o block and c_proj block
     int fault_step;  // test hook: >= 0 makes the last CU abort at that step as a timed-out wait would
     int coop;        // launch cooperatively (co-residency guaranteed by the runtime)
+    int gather_pause;  // loaders pause while the comm wave waits on a hand-off (C_GATHER)
+    int pad_args;
     int exp_att[8], exp_mlp[8];  // contributions each residual copy receives (attention / MLP CUs)
     float eps, penalty;
 };
@@ -162,7 +164,12 @@ __host__ __device__ inline Lay lds_layout(int D, int R, int max_nq, int swl, int
 }
 
 // ctl words
-enum { C_READY = 0, C_ABORT = 2, C_DONE = 3, C_CONT = 4, C_LOADED = 8, C_PHDONE = 16, C_CONS = 24, C_MID = 32 };
+enum { C_READY = 0, C_ABORT = 2, C_DONE = 3, C_CONT = 4, C_GATHER = 5, C_LOADED = 8, C_PHDONE = 16, C_CONS = 24,
+       C_MID = 32 };
+// C_GATHER: the comm wave is waiting on a hand-off (residual edge, q/k/v granules): the loaders
+// issue no new weight batches meanwhile, so the poll's loads do not queue behind this CU's own
+// refill burst (MI355X_MICROARCH.md "gather-pass": 1.0-1.7 us behind an unthrottled refill vs
+// 0.3-0.65 with the CU's own DMA quiet).  Args::gather_pause (DLMS_DF_GATHER_PAUSE=0: off, A/B).
 // (C_LOADED + j: loader wave j's completed-batch count)
 // row state words (st[b * 8 + k])
 enum { S_TOK = 0, S_POS = 1, S_FIN = 2, S_LEN = 3, S_SLOT = 4 };
@@ -340,6 +347,7 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
     int ec[COPIES];
 #pragma unroll
     for (int c = 0; c < COPIES; ++c) ec[c] = expc[c];
+    if (a.gather_pause) lds_st(ctl + C_GATHER, 1u);
     const u64 t0 = clk();
     // phase 1: poll ONE word per copy -- the element every producer adds last (row R-1, element
     // D-1) -- so 256 pollers do not hammer the lines the atomics are still updating
@@ -393,7 +401,10 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
                     pending &= ~(1u << (c * R + r));
                 }
             }
-        if (!pending) return true;
+        if (!pending) {
+            if (a.gather_pause) lds_st(ctl + C_GATHER, 0u);
+            return true;
+        }
         if ((unsigned)__builtin_amdgcn_readfirstlane((int)gld32(a.err)) || lds_ld(ctl + C_ABORT)) {
             lds_st(ctl + C_ABORT, 1u);
             return false;
@@ -527,6 +538,7 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
             if (cu.ah >= 0) {
                 const u64* g = sw + sc.qkv0 + (size_t)l * R * D3;
                 const int h = cu.ah;
+                if (a.gather_pause) lds_st(ctl + C_GATHER, 1u);
                 const u64 t0 = clk();
                 for (;;) {
                     bool all = true;
@@ -551,6 +563,7 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
                     __builtin_amdgcn_s_sleep(1);
                 }
                 if (!ok) break;
+                if (a.gather_pause) lds_st(ctl + C_GATHER, 0u);
                 stamp(a, s, l, 5, lane);
                 pid = pid_of(s, l, 1, L);
                 lds_st(ctl + C_READY, pid);
@@ -745,7 +758,7 @@ __device__ __forceinline__ void loader_wave(const Args& a, const Cu& cu, char* l
             const unsigned c = lds_ld(ctl + C_CONS + w);
             cons = c < cons ? c : cons;
         }
-        if ((b + 1) * BATCH > cons * 16u + RB) {  // ring full: publish everything, then wait
+        if ((b + 1) * BATCH > cons * 16u + RB || lds_ld(ctl + C_GATHER)) {  // ring full / a hand-off in progress
             drain();
             if (published != k) {
                 published = k;
@@ -871,42 +884,57 @@ __device__ __forceinline__ f32x4_t mfma_rows16(const char* ring, unsigned gro, u
 // this wave's 16-row output tiles t = w, w + NC, ... (t < ntiles) of a K-major block [16 ntiles][KP]
 // at ring offset bro (bro < RB): out[m][o0 + 16 t + l] = sum_k A[m][k] * Blk[16 t + l][k]
 // (v_mfma_f32_16x16x16_bf16 per 16-deep k block; afr[kb]: this lane's A fragment, row l & 15,
-// k = 16 kb + 4 (l >> 4) .. + 4); results go to part[m][o0 + ..] (lanes < 16).  Tiles go U at a
-// time (U = 3), all their B fragments read before their MFMAs: a whole-block unroll kept up to D / 64 f32x4
-// accumulators live and pushed the kernel past 256 VGPRs into scratch (r4: 768-wide batch 1 from
-// 30 to 51 ms; U = 4 spills too), fewer left the LDS latency exposed.  Offsets stay below 2 RB (a
-// block is smaller than the ring), so one conditional subtract wraps them -- no integer division.
-template <int D, int R, int KB, int U = 3>
-__device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsigned RB, int KP, int nkb, int ntiles,
-                                           int o0, const bf16x4_t (&afr)[KB], float* part, int w, int lane) {
+// k = 16 kb + 4 (l >> 4) .. + 4); results go to part[m][o0 + ..] (lanes < 16).
+// Tiles go U = 3 at a time with every B fragment of the group read before its MFMAs, and NO
+// branch between those reads: a tile index past the end is clamped to the last tile (a valid
+// ring address, its result discarded) -- a branch per read made the compiler wait for each
+// (s_waitcnt lgkmcnt(0) at every join) and serialised the whole block (r4 trace: W_o 1.4 -> 4.8 us);
+// NKB is a template constant for the same reason.  A whole-block unroll kept D / 64 f32x4
+// accumulators live and pushed the kernel past 256 VGPRs into scratch.  Offsets stay below
+// 2 RB (a block is smaller than the ring), so one conditional subtract wraps them.
+template <int D, int R, int NKB, int U = 3>
+__device__ __forceinline__ void mfma_block_k(const char* ring, unsigned bro, unsigned RB, int KP, int ntiles, int o0,
+                                             const bf16x4_t* afr, float* part, int w, int lane) {
     const int n = lane & 15, kq = lane >> 4;
     const unsigned base = bro + (unsigned)((16 * w + n) * KP + 4 * kq) * 2u;
     const unsigned tstep = (unsigned)(16 * NC * KP) * 2u;
-    for (int j = 0; w + NC * j < ntiles; j += U) {
-        bf16x4_t b[U][KB];
+    const int mine = ntiles > w ? (ntiles - 1 - w) / NC + 1 : 0;  // tiles of this wave (uniform)
+    for (int j = 0; j < mine; j += U) {
+        bf16x4_t b[U][NKB];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
+            const int jj = j + u < mine ? j + u : mine - 1;
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb)
-                if (kb < nkb && w + NC * (j + u) < ntiles)
-                    b[u][kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * (j + u) + 32u * kb, RB));
+            for (int kb = 0; kb < NKB; ++kb)
+                b[u][kb] = *reinterpret_cast<const bf16x4_t*>(ring + ring_wrap(base + tstep * jj + 32u * kb, RB));
+        }
         f32x4_t acc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
+        for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (kb < nkb && w + NC * (j + u) < ntiles)
-                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b[u][kb], acc[u], 0, 0, 0);
+            for (int u = 0; u < U; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(afr[kb], b[u][kb], acc[u], 0, 0, 0);
         if (lane < 16) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (w + NC * (j + u) < ntiles) {
+                if (j + u < mine) {
 #pragma unroll
                     for (int r = 0; r < R; ++r) part[r * D + o0 + 16 * (w + NC * (j + u)) + lane] = acc[u][r];
                 }
         }
+    }
+}
+
+template <int D, int R, int KB>
+__device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsigned RB, int KP, int nkb, int ntiles,
+                                           int o0, const bf16x4_t (&afr)[KB], float* part, int w, int lane) {
+    static_assert(KB == 4, "k blocks");
+    switch (nkb) {  // (uniform: the block's K from the host table)
+        case 1: mfma_block_k<D, R, 1>(ring, bro, RB, KP, ntiles, o0, afr, part, w, lane); break;
+        case 2: mfma_block_k<D, R, 2>(ring, bro, RB, KP, ntiles, o0, afr, part, w, lane); break;
+        case 3: mfma_block_k<D, R, 3>(ring, bro, RB, KP, ntiles, o0, afr, part, w, lane); break;
+        default: mfma_block_k<D, R, 4>(ring, bro, RB, KP, ntiles, o0, afr, part, w, lane); break;
     }
 }
 
@@ -916,17 +944,17 @@ __device__ __forceinline__ void mfma_block(const char* ring, unsigned bro, unsig
 template <int KB, int R>
 __device__ __forceinline__ void load_afr(const bf16_t* hb, int k0, int nvalid, int nkb, bf16x4_t (&afr)[KB],
                                          int lane) {
+    // every read unconditional (row clamped, k blocks past the end read LDS that lies further
+    // on and are masked to zero) so the reads issue back to back; masking by select, no branch
     const int m = lane & 15, kq = lane >> 4;
+    const bf16_t* row = hb + (m < R ? m : R - 1) * 64 + k0 + 4 * kq;
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
-        bf16x4_t v = {0, 0, 0, 0};
-        if (kb < nkb && m < R) {
-            v = *reinterpret_cast<const bf16x4_t*>(hb + m * 64 + k0 + 16 * kb + 4 * kq);
+        const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(row + 16 * kb);
+        bf16x4_t z;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (16 * kb + 4 * kq + j >= nvalid) v[j] = 0;
-        }
-        afr[kb] = v;
+        for (int j = 0; j < 4; ++j) z[j] = (kb < nkb && m < R && 16 * kb + 4 * kq + j < nvalid) ? v[j] : (short)0;
+        afr[kb] = z;
     }
 }
 
@@ -1280,7 +1308,10 @@ __device__ __forceinline__ void compute_wave(const Args& a, const Cu& cu, char* 
 template <int D, int R, int PFG>
 __global__ __launch_bounds__(NTHREADS, 1) void dataflow_decode_kernel(Args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index as a wave-uniform (scalar) value: every role branch and every "this wave's
+    // tiles" loop bound derived from it is then a scalar branch, not an exec mask (a VGPR-derived
+    // bound made mfma_block's tile loop exec-masked and serialised its LDS reads: r4 trace)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Cu cu = a.cus[blockIdx.x];
     const Lay ly = lds_layout(D, R, a.max_nq, a.swl, a.ring_bytes);
     unsigned* ctl = reinterpret_cast<unsigned*>(smem + ly.ctl);

@@ -42,7 +42,7 @@ class DfLayer(ctypes.Structure):
 
 
 _INT_FIELDS = ("R", "D", "H", "L", "V", "T", "seen_words", "eos", "nsteps", "A", "C", "max_nq", "swl", "ring_bytes",
-               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop")
+               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop", "gather_pause", "pad_args")
 
 
 class DfArgs(ctypes.Structure):
@@ -392,6 +392,7 @@ class DataflowDecoder:
         a.ko, a.kf = self.ko, self.kf
         a.fault_step, self._fault_step = self._fault_step, -1
         a.coop = int(self.coop)
+        a.gather_pause = int(os.environ.get("DLMS_DF_GATHER_PAUSE", "1") != "0")
         for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
             a.exp_mlp[c] = self._exp_mlp[c]
             a.exp_att[c] = self._exp_att[c]
