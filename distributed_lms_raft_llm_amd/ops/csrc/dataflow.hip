@@ -372,35 +372,40 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    // phase 2: the whole buffer (almost always complete by now), one (row, copy) slab of EPL words
-    // at a time: a slab whose words all carry their final count is final for good (the buffer is
-    // fresh per step), so it is added to xs at once and never read again -- only EPL words are
-    // live per pass (all COPIES x R x EPL of them at once pushed the 2-row kernel into scratch)
-    unsigned pending = (1u << (COPIES * R)) - 1u;
+    // phase 2: the whole buffer (almost always complete by now), one ROW at a time: all COPIES x
+    // EPL words of the row in flight together (one round trip); a row whose words all carry their
+    // final count is final for good (the buffer is fresh per step), so it is added to xs at once
+    // and never read again -- holding every row's words at once pushed the 2-row kernel into scratch
+    unsigned pending = (1u << R) - 1u;
     for (;;) {
 #pragma unroll
-        for (int c = 0; c < COPIES; ++c)
+        for (int r = 0; r < R; ++r) {
+            if (!(pending & (1u << r))) continue;
+            u64 v[COPIES][EPL];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!(pending & (1u << (c * R + r)))) continue;
-                u64 v[EPL];
+            for (int c = 0; c < COPIES; ++c)
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) {
                     const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (((c * R + r) * D) + lane + 64 * i) * 8, 0,
                                                                         16 /* sc1 */);
-                    v[i] = ((u64)x[1] << 32) | x[0];
+                    v[c][i] = ((u64)x[1] << 32) | x[0];
                 }
-                bool ok = true;
+            bool ok = true;
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) ok &= (int)(v[i] >> 56) == ec[c];
-                if (__all(ok)) {
+            for (int c = 0; c < COPIES; ++c)
 #pragma unroll
-                    for (int i = 0; i < EPL; ++i)
-                        xs[r * D + lane + 64 * i] += (i64)(v[i] & CNT_MASK) - (i64)ec[c] * CNT_BIAS +
-                                                     (c == 0 ? f2fix(bias[i]) : 0);
-                    pending &= ~(1u << (c * R + r));
+                for (int i = 0; i < EPL; ++i) ok &= (int)(v[c][i] >> 56) == ec[c];
+            if (__all(ok)) {
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) {
+                    i64 t = f2fix(bias[i]);
+#pragma unroll
+                    for (int c = 0; c < COPIES; ++c) t += (i64)(v[c][i] & CNT_MASK) - (i64)ec[c] * CNT_BIAS;
+                    xs[r * D + lane + 64 * i] += t;
                 }
+                pending &= ~(1u << r);
             }
+        }
         if (!pending) {
             if (a.gather_pause) lds_st(ctl + C_GATHER, 0u);
             return true;
@@ -415,6 +420,31 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
             return false;
         }
         __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Publish this CU's part[r][o0 .. o0 + on) as counted fixed-point atomics into X (the residual-update
+// buffer of its copy): every LDS value read first (clamped index, no branch: one LDS round trip for
+// the lot), then the atomics (predicated only when the CU publishes a column range, on < D)
+template <int D, int R>
+__device__ __forceinline__ void publish(u64* X, const float* part, int o0, int on, int lane) {
+    constexpr int EPL = D / 64;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float p[EPL];
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) {
+            const int e = lane + 64 * i;
+            p[i] = part[r * D + o0 + (e < on ? e : on - 1)];
+        }
+        if (on == D) {
+#pragma unroll
+            for (int i = 0; i < EPL; ++i) gadd64(X + (size_t)r * D + lane + 64 * i, counted(f2fix(p[i])));
+        } else {
+#pragma unroll
+            for (int i = 0; i < EPL; ++i)
+                if (lane + 64 * i < on) gadd64(X + (size_t)r * D + lane + 64 * i, counted(f2fix(p[i])));
+        }
     }
 }
 
@@ -569,14 +599,7 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
                 lds_st(ctl + C_READY, pid);
                 if (!(ok = wait_phdone(ctl, pid, a, s))) break;
                 stamp(a, s, l, 6, lane);
-                u64* X = sw + (2 * l) * sc.xw + (size_t)cu.acp * R * D + cu.ao0;
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-#pragma unroll
-                    for (int i = 0; i < EPL; ++i) {
-                        const int e = lane + 64 * i;
-                        if (e < cu.aon) gadd64(X + (size_t)r * D + e, counted(f2fix(part[r * D + cu.ao0 + e])));
-                    }
+                publish<D, R>(sw + (2 * l) * sc.xw + (size_t)cu.acp * R * D + cu.ao0, part, cu.ao0, cu.aon, lane);
                 stamp(a, s, l, 7, lane);
             }
             // ---------------- E3: XA complete -> LN2 -> MLP
@@ -600,14 +623,7 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
             if (!(ok = wait_phdone(ctl, pid, a, s))) break;
             stamp(a, s, l, 10, lane);
             {
-                u64* X = sw + (2 * l + 1) * sc.xw + (size_t)cu.mcp * R * D + cu.pd0;
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-#pragma unroll
-                    for (int i = 0; i < EPL; ++i) {
-                        const int e = lane + 64 * i;
-                        if (e < cu.pdn) gadd64(X + (size_t)r * D + e, counted(f2fix(part[r * D + cu.pd0 + e])));
-                    }
+                publish<D, R>(sw + (2 * l + 1) * sc.xw + (size_t)cu.mcp * R * D + cu.pd0, part, cu.pd0, cu.pdn, lane);
                 stamp(a, s, l, 11, lane);
             }
         }
