@@ -141,13 +141,12 @@ def assign(d: int, n_head: int, n_inner: int, vocab_padded: int, G: int, GS: int
       CU adds d / J residual words per row instead of d (the per-CU atomic issue and the memory-side
       atomic count of the post-MLP edge shrink J-fold; the extra c_fc rows are prefetched weight
       bytes, off the critical path).  Slice i's contributions go to residual copy i % copies.
-    * Attention: each head on GS CUs, each computing the whole head.  ``attn_split="dims"`` (the
-      default): CU g owns head dims [g 64/GS, (g + 1) 64/GS) of W_o and publishes all d outputs
-      (contribution copy a % copies); ``"outputs"``: it owns all 64 dims and publishes the output
-      columns [g d/GS, (g + 1) d/GS) (copy h % copies) -- fewer atomics per CU, but measured
-      slower at GPT-2 widths (its W_o phase is longer, the edges did not shorten:
-      profiles/r4_df_partition_sweep.jsonl).  Attention CU a = h * GS + g sits at CU (a * G) // A,
-      spreading them over all XCDs.
+    * Attention: each head on GS CUs, each computing the whole head.  ``attn_split="dims"``: CU g
+      owns head dims [g 64/GS, (g + 1) 64/GS) of W_o and publishes all d outputs (contribution
+      copy a % copies, the round-3 split); ``"outputs"``: it owns all 64 dims and publishes the
+      output columns [g d/GS, (g + 1) d/GS) (copy h % copies) -- d / GS atomics per CU instead of
+      d.  (The decoder defaults to "outputs": profiles/r4_df_sweep_v4.jsonl.)  Attention CU
+      a = h * GS + g sits at CU (a * G) // A, spreading them over all XCDs.
     Every residual word then receives the same number of contributions per copy."""
     if n_head * GS > G or 64 % GS or (attn_split == "outputs" and d % (16 * GS)):
         raise ValueError(f"dataflow: GS={GS} does not split heads over {G} CUs")
@@ -261,7 +260,10 @@ class DataflowDecoder:
         cus = int(props.multi_processor_count)
         G = grid or int(os.environ.get("DLMS_DF_GRID", "0")) or min(cus * 25 // 32, 256)
         gs = gs or int(os.environ.get("DLMS_DF_GS", "2"))
-        split = os.environ.get("DLMS_DF_ATTN_SPLIT", "dims")
+        # each head's 2 attention CUs split W_o by OUTPUT columns (d / 2 residual words each): 29.3
+        # vs 30.5 ms at batch 1, 40.1 vs 41.4 at batch 2 against the head-dims split on one box
+        # (profiles/r4_df_sweep_v4.jsonl); DLMS_DF_ATTN_SPLIT=dims for the round-3 split
+        split = os.environ.get("DLMS_DF_ATTN_SPLIT", "outputs")
         while (cfg.n_head * gs > G or 64 % gs or (split == "outputs" and cfg.n_embd % (16 * gs))) and gs > 1:
             gs //= 2
         # MLP output groups J (see assign): 1 by default -- J = 2 / 4 (each CU publishing d / J

@@ -411,7 +411,7 @@ def main():
             if lms_m:
                 line["lms_nodes"] = {
                     a: {k: {q: round(v, 2) for q, v in m.get("histograms", {})[k].items() if q in ("count", "p50", "p99")}
-                        for k in ("gate_ms", "llm_answer_ms") if k in m.get("histograms", {})}
+                        for k in ("gate_ms", "gate_batch", "llm_answer_ms") if k in m.get("histograms", {})}
                     for a, m in lms_m.items()}
             print(json.dumps(line), flush=True)
             if args.out:
