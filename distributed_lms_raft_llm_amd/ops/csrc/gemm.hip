@@ -61,7 +61,16 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Synchronisation: counted `s_waitcnt vmcnt` + raw s_barrier (a __syncthreads() would drain the
 // in-flight DMA every step); out-of-range A rows read a clamped valid row (their results are never
 // stored), so the DMA never needs predication.
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN>
+//
+// MODE (big prefill GEMMs, 256x256 tiles; see launch_gemm_epi):
+//   bit 0  REGPF: a whole K-tile's fragments go LDS -> registers right after its barrier, so its
+//          buffer is free one barrier later and the DMA of tile t+2 is issued before tile t's
+//          MFMAs (two K-tiles of loads in flight with two LDS buffers, instead of one)
+//   bit 1  GROUPED: tiles enumerated in groups of GROUP_M row tiles x all column tiles, so the 32
+//          workgroups an XCD runs at once share 4 A panels and 8 W panels through its L2 (the
+//          column-major order gave every one of them its own A panel: 32 panels from beyond L2)
+#define GROUP_M 4
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN, int MODE = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __restrict__ A, int lda,
                                                       const void* __restrict__ W, int ldw, int M, int N,
                                                       int K, GemmEpi ep) {
@@ -97,8 +106,22 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
     const int bid0 = xcd_remap(blockIdx.x, nwg);
     const int split = bid0 / tiles;
     const int bid = bid0 - split * tiles;
-    const int tile_m = bid % tiles_m;
-    const int tile_n = bid / tiles_m;
+    constexpr bool REGPF = (MODE & 1) != 0;
+    constexpr bool GROUPED = (MODE & 2) != 0;
+    static_assert(!REGPF || (STAGES == 2 && IN == IN_BF16 && EPI != EPI_GELU_LN), "REGPF: 2 bf16 stages");
+    int tile_m, tile_n;
+    if constexpr (GROUPED) {
+        const int tiles_n = N / BN;
+        const int per_group = GROUP_M * tiles_n;
+        const int g = bid / per_group, r = bid - g * per_group;
+        const int gm0 = g * GROUP_M;
+        const int gsz = tiles_m - gm0 < GROUP_M ? tiles_m - gm0 : GROUP_M;
+        tile_m = gm0 + r % gsz;
+        tile_n = r / gsz;
+    } else {
+        tile_m = bid % tiles_m;
+        tile_n = bid / tiles_m;
+    }
     const int m0 = tile_m * BM;
     const int n0 = tile_n * BN;
     const int k_len = K / nsplit;
@@ -138,17 +161,57 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
     __shared__ float2 ln_stat[EPI == EPI_GELU_LN ? BM : 1];  // (mean, rstd) per tile row
 
     const int nk = k_len / BKE;
-    // prologue: up to STAGES-1 steps in flight; no step is ever loaded twice (short split-K slices
-    // would otherwise multiply their traffic)
-#pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) issue(s, s * BKE);
-
     const int frow = lane & 15;
     const int fk = lane >> 4;
     const int fsw = lane & 7;  // == row & 7 for every fragment row this lane reads
 
-    for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (REGPF) {
+        // tiles t and t+1 in flight at the top of iteration t; tile t+2 issued into tile t's buffer
+        // once every wave holds tile t's fragments in registers
+        issue(0, 0);
+        if (nk > 1) issue(1, BKE);
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk)
+                wait_vmcnt<PPW>();
+            else
+                wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();  // tile kt has landed for every lane
+            asm volatile("" ::: "memory");
+            const char* as = smem + (kt & 1) * STAGE_BYTES + (wm * WTM) * ROWB;
+            const char* ws = smem + (kt & 1) * STAGE_BYTES + A_BYTES + (wn * WTN) * ROWB;
+            bf16x8_t af[2][TM], bfr[2][TN];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int coff = (((ks * 4 + fk) ^ fsw) << 4);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    af[ks][i] = *reinterpret_cast<const bf16x8_t*>(as + (i * 16 + frow) * ROWB + coff);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    bfr[ks][j] = *reinterpret_cast<const bf16x8_t*>(ws + (j * 16 + frow) * ROWB + coff);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave's reads of buffer kt & 1 are done
+            asm volatile("" ::: "memory");
+            if (kt + 2 < nk) issue(kt & 1, (kt + 2) * BKE);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    // prologue: up to STAGES-1 steps in flight; no step is ever loaded twice (short split-K slices
+    // would otherwise multiply their traffic)
+    if constexpr (!REGPF) {
+#pragma unroll
+        for (int s = 0; s < STAGES - 1; ++s)
+            if (s < nk) issue(s, s * BKE);
+    }
+
+    for (int kt = 0; kt < (REGPF ? 0 : nk); ++kt) {
         // this lane's share of step kt has landed (steady state: STAGES-2 younger steps may stay in
         // flight; in the tail fewer were issued, so drain everything) ...
         if (nk - kt >= STAGES - 1)
@@ -438,7 +501,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 // counted when the launch is issued, so graph captures count once per capture)
 static std::atomic<long> g_tile_count[4][4];  // [BM 32/64/128/256][BN 64/96/128/256]
 
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN>
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN, int MODE = 0>
 static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
     g_tile_count[BM <= 32 ? 0 : BM <= 64 ? 1 : BM <= 128 ? 2 : 3][BN <= 64 ? 0 : BN <= 96 ? 1 : BN <= 128 ? 2 : 3]
@@ -449,12 +512,12 @@ static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw
     if (EPI != EPI_ARGMAX && EPI != EPI_F32 && EPI != EPI_F32X2 && stage_out > lds) lds = stage_out;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN, MODE>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN>), dim3(tiles), dim3(64 * WM * WN), lds, stream, A,
+    hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN, MODE>), dim3(tiles), dim3(64 * WM * WN), lds, stream, A,
                        lda, W,
                        ldw, M, N, K, ep);
     return hipGetLastError();
@@ -475,6 +538,15 @@ static bool gemm96_on() {
     }
     return v == 1;
 }  // tuning override (dlms_gemm_force_tile), -1 = heuristic
+// MODE of the big-M 256x256 GEMMs (prefill): DLMS_GEMM_BIG_MODE (0 plain, 1 REGPF, 2 GROUPED, 3 both)
+static int big_mode() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("DLMS_GEMM_BIG_MODE");
+        v = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+    }
+    return v;
+}
 
 template <int EPI, int IN>
 static hipError_t launch_forced(int id, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
@@ -523,6 +595,25 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
     // (not for the fp32 split-K epilogue: its 256 x 1 KiB staged rows exceed the LDS)
     if (N % 256 == 0 && id == 14 && EPI != EPI_PARTIAL)
         return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+    // big-GEMM modes (REGPF = 1, GROUPED = 2, both = 3)
+    if constexpr (IN == IN_BF16 && EPI != EPI_GELU_LN) {
+        if (N % 256 == 0 && EPI != EPI_PARTIAL) {
+            switch (id) {
+                case 20: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
+                case 21: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
+                case 22: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
+                default: break;
+            }
+        }
+        if (N % 128 == 0) {
+            switch (id) {
+                case 23: return launch_gemm_cfg<256, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
+                case 24: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
+                case 25: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
+                default: break;
+            }
+        }
+    }
     *done = false;
     return hipSuccess;
 }
@@ -544,8 +635,17 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     // QKV at M=8192 = 288 tiles loses 6 %)
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_QKV) {
         const long t256 = (long)((M + 255) / 256) * (N / 256);
-        if (N % 256 == 0 && M >= 4096 && (t256 <= 256 || t256 % 256 >= 128 || t256 >= 512))
+        if (N % 256 == 0 && M >= 4096 && (t256 <= 256 || t256 % 256 >= 128 || t256 >= 512)) {
+            if constexpr (IN == IN_BF16) {
+                switch (big_mode()) {
+                    case 1: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
+                    case 2: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
+                    case 3: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
+                    default: break;
+                }
+            }
             return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
+        }
     }
     // (LM head on a 512-row decode half: 256x256 tiles are 86.4 -> 78.3 us alone (N = 50432,
     // profiles/r1_gemm_256tile.jsonl) but 1 % slower in the two-stream decode step, where the

@@ -17,6 +17,7 @@
 #   skinny           latency-path kernel microbench                -> gpurun_out/skinny.jsonl
 #   attn             split-K flash-decode sweep (B x T x waves x workgroups)   -> gpurun_out/attn.jsonl
 #   pgemm            packed-prefill GEMMs (32768 rows) vs hipBLASLt -> gpurun_out/pgemm.jsonl
+#   pgemmt:<ids>     the same plus forced tile configs (dlms_gemm_force_tile ids, ',')
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
@@ -100,6 +101,9 @@ for task in "$@"; do
                    step 300 gpurun_out/skinny_cold.jsonl python -u scripts/bench_skinny.py --batches 1 --cold-mb 512 --T 150 ;;
         attn) step 300 gpurun_out/attn.jsonl python -u scripts/bench_skinny.py --attn-only --batches 1,8,32 --T 150,1024 ;;
         pgemm) step 300 gpurun_out/pgemm.jsonl python -u scripts/bench_prefill_gemm.py; grep '^{' gpurun_out/pgemm.jsonl ;;
+        pgemmt:*)  # pgemmt:<tile ids, ','>  the same plus forced tile configs (max rel err vs fp32 each)
+            step 400 gpurun_out/pgemm.jsonl python -u scripts/bench_prefill_gemm.py --tiles "${task#pgemmt:}"
+            grep '^{' gpurun_out/pgemm.jsonl ;;
         conc) step 300 gpurun_out/conc.jsonl python -u scripts/bench_concurrency.py; grep '^{' gpurun_out/conc.jsonl ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
         gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;

@@ -124,6 +124,47 @@ def test_gemm_256_tiles_large_m(epi):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25])
+@pytest.mark.parametrize("epi", ["gelu_tanh", "qkv"])
+def test_gemm_big_modes(tile, epi):
+    """The big-GEMM main-loop modes (gemm.hip MODE: REGPF = fragments of a whole K-tile in registers,
+    DMA two K-tiles ahead; GROUPED = tiles in groups of 4 row tiles) on 256x256 (ids 20-22),
+    256x128 (23) and 128x128 (24, 25) tiles, forced, vs fp32.  M = 4100 leaves a partial last row
+    tile and a partial last tile group; the QKV scatter covers the epilogue that the prefill uses."""
+    ops = _ops()
+    L = ops.lib()
+    M, K = 4100, 768
+    L.dlms_gemm_force_tile(tile)
+    try:
+        if epi == "qkv":
+            H, S = 4, 5
+            D = H * 64
+            T = 1024
+            a, w = _bf(M, D, seed=61), _bf(3 * D, D, scale=0.05, seed=62)
+            bias = torch.randn(3 * D, device=DEV)
+            q = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+            kc = torch.zeros(S, H, T, 64, dtype=torch.bfloat16, device=DEV)
+            vc = torch.zeros_like(kc)
+            slot = (torch.arange(M, device=DEV) // T).to(torch.int32)
+            pos = (torch.arange(M, device=DEV) % T).to(torch.int32)
+            ops.gemm(a, w, ops.EPI_QKV, bias=bias, q_out=q, k_cache=kc, v_cache=vc, row_slot=slot, row_pos=pos)
+            ref = a.float() @ w.float().t() + bias
+            torch.testing.assert_close(q.float(), ref[:, :D], atol=2e-2, rtol=2e-2)
+            sl, ps = slot.long(), pos.long()
+            torch.testing.assert_close(kc[sl, :, ps].reshape(M, D).float(), ref[:, D:2 * D], atol=2e-2, rtol=2e-2)
+            torch.testing.assert_close(vc[sl, :, ps].reshape(M, D).float(), ref[:, 2 * D:], atol=2e-2, rtol=2e-2)
+        else:
+            N = 3072
+            a, w = _bf(M, K, seed=63), _bf(N, K, scale=0.05, seed=64)
+            bias = torch.randn(N, device=DEV) * 0.1
+            out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+            ops.gemm(a, w, ops.EPI_GELU_TANH, bias=bias, out=out)
+            ref = torch.nn.functional.gelu(a.float() @ w.float().t() + bias, approximate="tanh")
+            torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    finally:
+        L.dlms_gemm_force_tile(-1)
+
+
 @pytest.mark.parametrize("epi,M,N,K", [("gelu_tanh", 256, 6400, 1600), ("bf16", 300, 4096, 1024),
                                         ("qkv", 256, 3072, 1024)])
 def test_gemm_wide_model_tiles(epi, M, N, K):
