@@ -27,6 +27,7 @@ Engine protocol (``HipGPT2Engine`` implements it; tests use a CPU fake):
 from __future__ import annotations
 
 import heapq
+import os
 import threading
 import time
 from collections import deque
@@ -143,6 +144,12 @@ class ContinuousBatcher:
             dev = getattr(self.engine, "device", None)
             if dev is not None and getattr(dev, "type", None) == "cuda" and dev.index is not None:
                 torch.cuda.set_device(dev)
+            prio = os.environ.get("DLMS_BATCHER_STREAM_PRIORITY")
+            if prio and dev is not None and getattr(dev, "type", None) == "cuda":
+                # serving beside other GPU processes on the same device (the LMS nodes' relevance
+                # gates): the decode chunks go on a stream of this priority (lower = higher;
+                # graphs are captured from it, so their replays inherit it)
+                torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=int(prio)))
             with torch.no_grad():
                 self._loop()
         except BaseException as e:  # fail every waiter loudly instead of hanging them

@@ -605,6 +605,13 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
                 default: break;
             }
         }
+        // all rows of a decode half in one row tile (the LM head: W streamed once, A re-read from L2)
+        switch (id) {
+            case 26: return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 0>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 27: return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
+            case 28: return launch_gemm_cfg<256, 64, 4, 1, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
+            default: break;
+        }
         if (N % 128 == 0) {
             switch (id) {
                 case 23: return launch_gemm_cfg<256, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);

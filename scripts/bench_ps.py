@@ -20,7 +20,10 @@ def main():
     ap.add_argument("--batches", default="256,512,1024")
     ap.add_argument("--cold-mb", type=int, default=512)
     ap.add_argument("--ops", default="qkv,fc,oproj,proj,lmhead")
+    ap.add_argument("--tiles", default="", help="forced tiled-GEMM configs to time too (dlms_gemm_force_tile ids)")
     args = ap.parse_args()
+    forced = [int(t) for t in args.tiles.split(",") if t.strip()]
+    L = ops.lib()
     dev, D = "cuda", args.d
     shapes = {"qkv": (3 * D, D, ops.EPI_QKV), "fc": (4 * D, D, ops.EPI_GELU_TANH), "oproj": (D, D, ops.EPI_PARTIAL),
               "proj": (D, 4 * D, ops.EPI_PARTIAL), "lmhead": (50304, D, ops.EPI_ARGMAX)}
@@ -62,6 +65,14 @@ def main():
                 res[f"ps_s{s}"] = graph_time(lambda i: ops.gemm_ps(a, wsh[i % copies], epi, **kw, **ex))
                 if epi == ops.EPI_PARTIAL or s == 1:
                     res[f"tiled_s{s}"] = graph_time(lambda i: ops.gemm(a, ws[i % copies], epi, **kt, **ex))
+            for t in forced:
+                if epi == ops.EPI_PARTIAL:
+                    continue
+                L.dlms_gemm_force_tile(t)
+                try:
+                    res[f"tile{t}"] = graph_time(lambda i: ops.gemm(a, ws[i % copies], epi, **kt))
+                finally:
+                    L.dlms_gemm_force_tile(-1)
             if epi == ops.EPI_ARGMAX:
                 for mt, nt in ((4, 1), (2, 2), (2, 1)):
                     rb = -(-M // (16 * mt))

@@ -21,7 +21,7 @@
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
-#   grpc:<tgt>:<rates> scripts/bench_grpc.py --target tutoring|lms at those offered q/s -> gpurun_out/grpc.jsonl
+#   grpc:<tgt>:<rates>[:<ENV=v,..>] scripts/bench_grpc.py --target tutoring|lms at those offered q/s -> gpurun_out/grpc.jsonl
 #   e2e:<n>          scripts/run_config.py --config n (Raft cluster + gate + tutor) -> gpurun_out/e2e_<n>.log
 #   e2e1:<n>         the same with the tutor at TP=1 (one-GPU boxes: configs 4/5 ask for TP=4/8)
 #   sweep:<ENV=v,..> one bench.py run per ';'-separated env set   -> gpurun_out/sweep.jsonl
@@ -129,10 +129,12 @@ for task in "$@"; do
             spec=${task#dfsweep:}
             step 900 gpurun_out/dfsweep.log bash scripts/df_sweep.sh -o gpurun_out/df_sweep.jsonl ${spec//;/ }
             tail -12 gpurun_out/dfsweep.log ;;
-        grpc:*)  # grpc:<tutoring|lms>:<rates>  sustained open-loop gRPC serving -> gpurun_out/grpc.jsonl
-            spec=${task#grpc:}; tgt=${spec%%:*}; rates=${spec#*:}
-            step 600 gpurun_out/grpc.log python -u scripts/bench_grpc.py --target "$tgt" --rates "$rates" --duration 20 \
-                --warmup 8 --client-procs 8 --out gpurun_out/grpc.jsonl --log gpurun_out/grpc_server.log
+        grpc:*)  # grpc:<tutoring|lms>:<rates>[:<ENV=v,...>]  sustained open-loop gRPC serving -> gpurun_out/grpc.jsonl
+            spec=${task#grpc:}; tgt=${spec%%:*}; rest=${spec#*:}; rates=${rest%%:*}; envs=""
+            if [ "$rest" != "$rates" ]; then envs=${rest#*:}; fi
+            step 600 gpurun_out/grpc.log env ${envs//,/ } python -u scripts/bench_grpc.py --target "$tgt" --rates "$rates" \
+                --duration 20 --warmup 8 --client-procs 8 --out gpurun_out/grpc.jsonl --log gpurun_out/grpc_server.log \
+                --tag "$envs"
             tail -2 gpurun_out/grpc.jsonl | cut -c1-400 ;;
         e2e:*) step 900 gpurun_out/e2e_${task#e2e:}.log python -u scripts/run_config.py --config ${task#e2e:}
                tail -3 gpurun_out/e2e_${task#e2e:}.log ;;

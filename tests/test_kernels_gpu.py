@@ -194,12 +194,24 @@ def test_gemm_wide_model_tiles(epi, M, N, K):
     torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [1, 5, 32, 37, 512])
-def test_gemm_argmax_penalty(M):
+@pytest.mark.parametrize("M,tile", [(1, -1), (5, -1), (32, -1), (37, -1), (512, -1), (512, 26), (512, 27),
+                                    (300, 27), (512, 28)])
+def test_gemm_argmax_penalty(M, tile):
     """Fused penalty + argmax epilogue vs fp32.  The key buffer is pre-filled with huge stale keys,
     which a tile wider than 64 columns must zero in every 64-column group it covers (a narrower
-    earlier config could have left keys there)."""
+    earlier config could have left keys there).  ``tile``: forced LM-head tiles with all rows of
+    a decode half in one row tile (512x64, plain and register-staged; 256x64)."""
     ops = _ops()
+    if tile >= 0:
+        ops.lib().dlms_gemm_force_tile(tile)
+        try:
+            return _argmax_case(ops, M)
+        finally:
+            ops.lib().dlms_gemm_force_tile(-1)
+    _argmax_case(ops, M)
+
+
+def _argmax_case(ops, M):
     K, V = 768, 50257
     Vp = (V + 63) // 64 * 64
     a = _bf(M, K, seed=9)
