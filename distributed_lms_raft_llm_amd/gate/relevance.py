@@ -51,6 +51,9 @@ class RelevanceGate:
         self.passes = 0
         self.batched_queries = 0
         self._last_pass_s = 0.0  # duration of the previous encoder pass (adaptive batching window)
+        # cap of that adaptive wait (DLMS_GATE_MAX_WAIT_MS): longer = fewer, larger passes beside
+        # the tutoring decode on a shared GPU, at that much more gate latency
+        self.max_wait_s = float(os.environ.get("DLMS_GATE_MAX_WAIT_MS", "8")) / 1e3
         self._last_end = 0.0
 
     @classmethod
@@ -129,14 +132,14 @@ class RelevanceGate:
                 while not self._pending:
                     self._pcv.wait()
                 # the first query waits for company: window_s when the gate was idle, but under
-                # load as long as the previous pass took (capped at 8 ms) -- queries keep arriving
+                # load as long as the previous pass took (capped at max_wait_s) -- queries keep arriving
                 # during a pass anyway, and every pass is a chain of small kernels that competes with
                 # the tutoring decode for the same GPU, so one pass per several queries is the point
                 # (serving bench: 1 ms windows gave ~1 query per pass at 1.2 k q/s per node and
                 # slowed the co-located tutor's decode ~2x)
                 now = time.monotonic()
                 busy = now - self._last_end < 0.05
-                wait = min(max(self.window_s, self._last_pass_s if busy else 0.0), 0.008)
+                wait = min(max(self.window_s, self._last_pass_s if busy else 0.0), self.max_wait_s)
                 end = now + wait
                 while len(self._pending) < self.max_batch and time.monotonic() < end:
                     self._pcv.wait(max(0.0, end - time.monotonic()))

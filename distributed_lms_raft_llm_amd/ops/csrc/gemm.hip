@@ -538,12 +538,14 @@ static bool gemm96_on() {
     }
     return v == 1;
 }  // tuning override (dlms_gemm_force_tile), -1 = heuristic
-// MODE of the big-M 256x256 GEMMs (prefill): DLMS_GEMM_BIG_MODE (0 plain, 1 REGPF, 2 GROUPED, 3 both)
+// big-M GEMMs (prefill): unset -> 128x128 tiles with MODE 3; DLMS_GEMM_BIG_MODE=0..3 -> the
+// 256x256 tile with that MODE (0 plain, 1 REGPF, 2 GROUPED, 3 both), the A/B of
+// profiles/r4_prefill_gemm_modes.jsonl
 static int big_mode() {
-    static int v = -1;
-    if (v < 0) {
+    static int v = -2;
+    if (v == -2) {
         const char* e = getenv("DLMS_GEMM_BIG_MODE");
-        v = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+        v = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
     }
     return v;
 }
@@ -636,6 +638,18 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     }
     const long t64 = (long)((M + 63) / 64) * (N / 64) * split;
     const long t128 = (long)((M + 127) / 128) * (N / 128) * split;
+    // big prefill GEMMs (1024 prompts x 32 tokens = 32768 rows): 128x128 tiles with a whole K-tile
+    // of fragments in registers (the DMA two K-tiles ahead) and tiles in groups of 4 row tiles (the
+    // 32 workgroups an XCD runs at once share their A and W panels in its L2); two workgroups per
+    // CU, so one's epilogue runs under the other's K loop.  profiles/r4_prefill_gemm_modes.jsonl at
+    // M = 32768: QKV 180.2 -> 153.5 us (256x256 tiles before), out-projection 82.4 -> 66.1, c_proj
+    // 199.6 -> 172.3, c_fc with a plain bf16 epilogue 206.1 -> 199.4 (hipBLASLt, plain bf16 out:
+    // 146.0 / 64.7 / 139.9 / 148.4)
+    if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF ||
+                                    EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
+        if (big_mode() < 0 && M >= 4096 && N % 128 == 0)
+            return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
+    }
     // big prefill GEMMs with a bf16 epilogue: 256x256 tiles, 8 waves of 128x64 (one workgroup per
     // CU: its 128 KiB ring + 135 KiB staged epilogue), unless the last round of tiles would run
     // nearly empty (profiles/r1_gemm_256tile.jsonl: c_fc M=32768 247 -> 192 us, QKV 184 -> 154 us;
@@ -645,6 +659,7 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
         if (N % 256 == 0 && M >= 4096 && (t256 <= 256 || t256 % 256 >= 128 || t256 >= 512)) {
             if constexpr (IN == IN_BF16) {
                 switch (big_mode()) {
+                    case 0: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
                     case 1: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
                     case 2: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
                     case 3: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);

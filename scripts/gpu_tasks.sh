@@ -19,6 +19,7 @@
 #   pgemm            packed-prefill GEMMs (32768 rows) vs hipBLASLt -> gpurun_out/pgemm.jsonl
 #   pgemmt:<ids>     the same plus forced tile configs (dlms_gemm_force_tile ids, ',')
 #   ps               panel-resident LM-head GEMM vs tiled          -> gpurun_out/ps.jsonl
+#   pst:<ids>        LM head at 512 rows, gemm_ps vs forced tiled configs
 #   gate             relevance gate under 100 concurrent GetLLMAnswer calls    -> gpurun_out/gate.jsonl
 #   serving          open-loop Poisson serving at 20 / 200 / 1000 queries/s      -> gpurun_out/serving.jsonl
 #   grpc:<tgt>:<rates>[:<ENV=v,..>] scripts/bench_grpc.py --target tutoring|lms at those offered q/s -> gpurun_out/grpc.jsonl
@@ -106,6 +107,9 @@ for task in "$@"; do
             grep '^{' gpurun_out/pgemm.jsonl ;;
         conc) step 300 gpurun_out/conc.jsonl python -u scripts/bench_concurrency.py; grep '^{' gpurun_out/conc.jsonl ;;
         ps) step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 256,512,1024 ;;
+        pst:*)  # pst:<tile ids, ','>  LM head at 512 rows: gemm_ps vs forced tiled configs
+            step 300 gpurun_out/ps.jsonl python -u scripts/bench_ps.py --ops lmhead --batches 512 --tiles "${task#pst:}"
+            grep '^{' gpurun_out/ps.jsonl ;;
         gate) step 300 gpurun_out/gate.jsonl python -u scripts/bench_gate.py --clients 100 --rounds 5 ;;
         serving5) step 300 gpurun_out/serving5.jsonl python -u scripts/bench_serving.py --rates 5 --queries 100 \
                       --modes continuous --prompt-jitter 0; grep '^{' gpurun_out/serving5.jsonl ;;
