@@ -359,9 +359,6 @@ class HipGPT2Engine:
                  64 * (2 * cfg.n_embd + 32) + 8 * 4096 <= ops.PS_LDS_BYTES and
                  os.environ.get("DLMS_PS_LMHEAD", "1") != "0")
         self.ps_lm = ps_lm and not self.w.fp8
-        # DLMS_LM_TILE512=1: 257-512-row LM heads on the tiled kernel's one-row-tile 512x64 config
-        # (gemm.hip) instead of gemm_ps
-        self.lm_tile512 = os.environ.get("DLMS_LM_TILE512", "0") == "1"
         if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
             # (the latency path's skinny LM head reads the same pre-shuffled copy)
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
@@ -644,8 +641,7 @@ class HipGPT2Engine:
         P = self.key_parts.shape[1]  # partial keys per row the LM head writes (and the consumer reads)
         if keys_ready:  # the caller ran the LM head (skinny, ln_f fused): one key per 64 columns
             P = self.lm_head_sh.shape[0] * 16 // 64
-        elif hidden.dtype != ops.FP8 and self.ps_lm and B >= self.PS_LM_MIN_ROWS and not (
-                self.lm_tile512 and 256 < B <= 512):
+        elif hidden.dtype != ops.FP8 and self.ps_lm and B >= self.PS_LM_MIN_ROWS:
             P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16, self.lm_head_sh.shape[1] * 32)
             ops.gemm_ps(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                         vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)

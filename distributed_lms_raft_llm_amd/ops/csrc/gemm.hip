@@ -538,14 +538,6 @@ static bool gemm96_on() {
     }
     return v == 1;
 }  // tuning override (dlms_gemm_force_tile), -1 = heuristic
-static bool lm_tile512_on() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("DLMS_LM_TILE512");
-        v = (e != nullptr && e[0] == '1') ? 1 : 0;
-    }
-    return v == 1;
-}
 // big-M GEMMs (prefill): unset -> 128x128 tiles with MODE 3; DLMS_GEMM_BIG_MODE=0..3 -> the
 // 256x256 tile with that MODE (0 plain, 1 REGPF, 2 GROUPED, 3 both), the A/B of
 // profiles/r4_prefill_gemm_modes.jsonl
@@ -615,7 +607,9 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
                 default: break;
             }
         }
-        // all rows of a decode half in one row tile (the LM head: W streamed once, A re-read from L2)
+        // all rows of a decode half in one row tile (the LM head: W streamed once, A re-read from
+        // L2) -- measured slower than gemm_ps at 512 rows: 89.3 / 73.3 (256x64) vs 67.9 us
+        // (profiles/r4_lmhead_tiles_m512.jsonl), kept as forced configs for the bench
         switch (id) {
             case 26: return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 0>(A, lda, W, ldw, M, N, K, ep, stream);
             case 27: return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
@@ -646,13 +640,6 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     }
     const long t64 = (long)((M + 63) / 64) * (N / 64) * split;
     const long t128 = (long)((M + 127) / 128) * (N / 128) * split;
-    // LM head of a 257-512-row decode half (DLMS_LM_TILE512): every row in ONE row tile (512x64, 8
-    // waves of 64x64, register-staged fragments), so the 77 MB of W stream from HBM once per call
-    // instead of once per 64-row panel
-    if constexpr (EPI == EPI_ARGMAX && IN == IN_BF16) {
-        if (lm_tile512_on() && M > 256 && M <= 512 && N >= 8192)
-            return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
-    }
     // big prefill GEMMs (1024 prompts x 32 tokens = 32768 rows): 128x128 tiles with a whole K-tile
     // of fragments in registers (the DMA two K-tiles ahead) and tiles in groups of 4 row tiles (the
     // 32 workgroups an XCD runs at once share their A and W panels in its L2); two workgroups per

@@ -266,11 +266,12 @@ class DataflowDecoder:
         split = os.environ.get("DLMS_DF_ATTN_SPLIT", "outputs")
         while (cfg.n_head * gs > G or 64 % gs or (split == "outputs" and cfg.n_embd % (16 * gs))) and gs > 1:
             gs //= 2
-        # MLP output groups J (see assign; each CU publishes d / J residual words of c_proj): 2 by
-        # default -- batch 1 28.7 vs 29.3 ms at J = 1 (profiles/r4_df_sweep_j2_outputs.jsonl; with
-        # the head-dims W_o split 32.4 vs 34.2, r4_df_partition_sweep.jsonl); J = 4 duplicates too
-        # many c_fc rows per CU (the MLP phase 2.4 -> 4.1 us in r4_df_trace_j4_vs_r3.txt)
-        j = j or int(os.environ.get("DLMS_DF_J", "2"))
+        # MLP output groups J (see assign; each CU publishes d / J residual words of c_proj): 2 at
+        # d 768 -- batch 1 28.7 vs 29.3 ms at J = 1 (profiles/r4_df_sweep_j2_outputs.jsonl; with the
+        # head-dims W_o split 32.4 vs 34.2, r4_df_partition_sweep.jsonl) -- 1 at d 1024 (GPT-2-medium
+        # 77.7 at J = 1 vs 82.7, r4_df_sweep_medium_j.jsonl: its CUs' c_fc rows double); J = 4
+        # duplicates too many c_fc rows (the MLP phase 2.4 -> 4.1 us, r4_df_trace_j4_vs_r3.txt)
+        j = j or int(os.environ.get("DLMS_DF_J", "2" if cfg.n_embd <= 768 else "1"))
         while j > 1 and (G % j or -(-eng.w.ffn_local * j // G) > 64 or cfg.n_embd % (16 * j)):
             j -= 1
         self.G, self.GS, self.J = G, gs, j
