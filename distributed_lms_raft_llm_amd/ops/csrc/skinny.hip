@@ -470,11 +470,18 @@ __device__ __forceinline__ void addln_rows_lds(const void* __restrict__ x_in, fl
             for (int c = 0; c < NV4; ++c) pv[i][s][c] = pr[cidx[c]];
         }
     }
+    // GPT-2-XL's fixed-point variant (d 1600, two int64 copies per element in flight) loads gamma /
+    // beta only once the residual is summed: held from the start they took it to 292 registers, one
+    // wave per SIMD, and its 300 QKV workgroups ran in two rounds on 256 CUs; the late load is one
+    // L2 round trip under the variance reduction.
+    constexpr bool LATE_GB = XFIX && NV4 >= 7;
     float4 gv[NV4], bv[NV4], rb[NV4];
 #pragma unroll
     for (int c = 0; c < NV4; ++c) {
-        gv[c] = reinterpret_cast<const float4*>(gamma)[cidx[c]];
-        bv[c] = reinterpret_cast<const float4*>(beta)[cidx[c]];
+        if constexpr (!LATE_GB) {
+            gv[c] = reinterpret_cast<const float4*>(gamma)[cidx[c]];
+            bv[c] = reinterpret_cast<const float4*>(beta)[cidx[c]];
+        }
         rb[c] = res_bias ? reinterpret_cast<const float4*>(res_bias)[cidx[c]] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     after_loads();
@@ -507,6 +514,16 @@ __device__ __forceinline__ void addln_rows_lds(const void* __restrict__ x_in, fl
                 if (valid[c]) reinterpret_cast<float4*>(v_lds + (size_t)row * K)[cidx[c]] = v[i][c];
         }
         const float mean = wave_sum(s) / (float)K;
+        if constexpr (LATE_GB) {
+            if (i == 0) {
+                asm volatile("" ::: "memory");  // issued here, not hoisted beside the residual loads
+#pragma unroll
+                for (int c = 0; c < NV4; ++c) {
+                    gv[c] = reinterpret_cast<const float4*>(gamma)[cidx[c]];
+                    bv[c] = reinterpret_cast<const float4*>(beta)[cidx[c]];
+                }
+            }
+        }
         float ss = 0.f;
 #pragma unroll
         for (int c = 0; c < NV4; ++c) {
@@ -667,7 +684,7 @@ extern "C" hipError_t dlms_skinny_addln_gemm(int epi, const void* x_in, float* x
                                              int N, int K, const GemmEpi* ep, int xfix, long long xcs, void* zero_buf,
                                              int zero_chunks, hipStream_t stream) {
     if (M <= 0 || M > dlms_skinny_addln_max_rows(K) || N % 16) return hipErrorInvalidValue;
-    if (xfix && (epi != SK_QKV || nsplit != 0 || x_out != nullptr)) return hipErrorInvalidValue;
+    if (xfix && (epi != SK_QKV || nsplit != 0 || x_out != nullptr || res_bias != nullptr)) return hipErrorInvalidValue;
     const AddlnArgs a{x_in, x_out, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps,
                       reinterpret_cast<const bf16_t*>(Wsh), M, N, K, reinterpret_cast<uint4*>(zero_buf),
                       zero_buf ? zero_chunks : 0, xcs};

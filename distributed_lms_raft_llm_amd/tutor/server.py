@@ -173,7 +173,7 @@ class TutoringServer:
 
             if engine.max_length != max_length:
                 raise ValueError("continuous batching: engine max_length differs from the server's")
-            self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk, stream_priority=-1)
+            self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
         else:
             self.batcher = Batcher(engine, self.gen, max_batch=max_batch, window_ms=window_ms)
         self.batching = batching
@@ -274,7 +274,7 @@ class AioTutoringServer(TutoringServer):
             raise ValueError("continuous batching: engine max_length differs from the server's")
         self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
         self.tok = tokenizer or GPT2BPE(eos_token_id=getattr(getattr(engine, "cfg", None), "eos_token_id", 50256))
-        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk, stream_priority=-1)
+        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
         self.batching = "continuous"
         self.engine = engine
         self._stopping = threading.Event()
@@ -328,7 +328,7 @@ class PooledTutoringServer(TutoringServer):
         if engine.max_length != max_length:
             raise ValueError("continuous batching: engine max_length differs from the server's")
         self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
-        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk, stream_priority=-1)
+        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
         self.batching = "continuous"
         self.engine = engine
         self.pool = pool

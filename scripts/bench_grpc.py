@@ -201,6 +201,11 @@ def _drain(proc, log):
 
 def start_tutor(args, log):
     env = dict(os.environ, PYTHONUNBUFFERED="1")
+    if args.target == "lms" and args.gate == "bert":
+        # the LMS nodes' BERT gates share the tutor's GPU: its decode chunks on a high-priority stream
+        # (LMS path at 3.5 k q/s p50 863 -> 606 ms; alone on the GPU the same setting cost the
+        # Tutoring path 16 % at 5.5 k q/s, so it is a co-location setting, not a default)
+        env.setdefault("DLMS_BATCHER_STREAM_PRIORITY", "-1")
     if args.engine == "null":
         cmd = [sys.executable, os.path.abspath(__file__), "--serve-null", "--max-length", str(args.max_length),
                "--null-slots", str(args.null_slots), "--null-step-ms", str(args.null_step_ms),

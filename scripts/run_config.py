@@ -154,7 +154,11 @@ def main():
                    "--master-addr=127.0.0.1", f"--master-port={master_port}"] + tut + ["--tp", str(cfg["tp"])]
         else:
             cmd = [sys.executable] + tut
-        tutor = Proc(cmd, os.path.join(work, "tutor.log"), env)
+        tenv = dict(env)
+        if cfg["gate"] == "bert" and cfg["device"] != "cpu":
+            # the LMS nodes' gates share the GPU: decode chunks on a high-priority stream (scripts/bench_grpc.py)
+            tenv.setdefault("DLMS_BATCHER_STREAM_PRIORITY", "-1")
+        tutor = Proc(cmd, os.path.join(work, "tutor.log"), tenv)
         procs.append(tutor)
         progress(f"config {args.config}: {cfg} -> {work}")
 
