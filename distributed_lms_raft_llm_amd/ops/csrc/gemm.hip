@@ -649,7 +649,9 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     // 146.0 / 64.7 / 139.9 / 148.4)
     if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF ||
                                     EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
-        if (big_mode() < 0 && M >= 4096 && N % 128 == 0)
+        // (only at the measured size class: 1024-prompt packed prefills; smaller admissions keep the
+        // tiles below, e.g. a 4096-row out-projection would put 192 128x128 tiles on 256 CUs)
+        if (big_mode() < 0 && M >= 16384 && N % 128 == 0)
             return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
     }
     // big prefill GEMMs with a bf16 epilogue: 256x256 tiles, 8 waves of 128x64 (one workgroup per

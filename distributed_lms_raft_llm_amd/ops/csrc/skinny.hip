@@ -436,7 +436,7 @@ struct NoOp {
 
 // (after_loads() runs once the activation loads are issued: a caller's own loads issued there stay in
 // flight under the LayerNorm instead of delaying it)
-template <int NSPLIT, int NV4, int RPW, bool XFIX, typename AfterLoads = NoOp>
+template <int NSPLIT, int NV4, int RPW, bool XFIX, bool LATE_GB = (XFIX && NV4 >= 7), typename AfterLoads = NoOp>
 __device__ __forceinline__ void addln_rows_lds(const void* __restrict__ x_in, float* __restrict__ x_out, int ldx,
                                                const float* __restrict__ parts, int ldp, long long split_stride,
                                                const float* __restrict__ res_bias, const float* __restrict__ gamma,
@@ -474,7 +474,6 @@ __device__ __forceinline__ void addln_rows_lds(const void* __restrict__ x_in, fl
     // beta only once the residual is summed: held from the start they took it to 292 registers, one
     // wave per SIMD, and its 300 QKV workgroups ran in two rounds on 256 CUs; the late load is one
     // L2 round trip under the variance reduction.
-    constexpr bool LATE_GB = XFIX && NV4 >= 7;
     float4 gv[NV4], bv[NV4], rb[NV4];
 #pragma unroll
     for (int c = 0; c < NV4; ++c) {
@@ -809,7 +808,9 @@ __global__ __launch_bounds__(256) void skinny_mlp_kernel(
     }
 
     // (1) residual rows -> LN2 -> LDS image (block 0 also keeps v); (2) c_fc slice on MFMA
-    addln_rows_lds<NSPLIT, NV4, RPW, XFIX>(x_in, nullptr, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, M,
+    // (gamma / beta with the residual loads here: one workgroup per CU either way, so the register
+    // saving of a late load would buy no occupancy, only a round trip)
+    addln_rows_lds<NSPLIT, NV4, RPW, XFIX, false>(x_in, nullptr, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, M,
                                            K, smem, ROWB, xcs, blockIdx.x == 0 ? v_lds : nullptr, issue_wp);
     __syncthreads();
     f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};

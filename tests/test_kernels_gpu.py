@@ -88,13 +88,15 @@ def test_gemm_qkv_scatter():
         torch.testing.assert_close(vc[s, :, p].float().reshape(-1), ref[m, 2 * D:], atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [4096, 16384])
 @pytest.mark.parametrize("epi", ["bf16", "gelu_tanh", "qkv"])
-def test_gemm_256_tiles_large_m(epi):
-    """Prefill-sized GEMMs (M >= 4096) take the big-GEMM path (128x128 tiles, register-staged
-    fragments, grouped tile order; asserted by the launch census): bias/GELU epilogues and the QKV
-    scatter (4096 packed rows over 4 slots x 1024 positions), vs fp32."""
+def test_gemm_256_tiles_large_m(epi, M):
+    """Prefill-sized GEMMs: 4096 rows take the 256x256 8-wave tile, the 1024-prompt packed prefill
+    size class (>= 16384 rows) the 128x128 register-staged grouped tiles (asserted by the launch
+    census): bias/GELU epilogues and the QKV scatter (packed rows over 4 slots), vs fp32."""
     ops = _ops()
-    M, K = 4096, 768
+    K = 768
+    tile = (256, 256) if M < 16384 else (128, 128)
     ops.gemm_tile_reset()
     if epi == "qkv":
         H, S = 4, 4
@@ -115,7 +117,7 @@ def test_gemm_256_tiles_large_m(epi):
         v_rows = vc.permute(0, 2, 1, 3).reshape(M, D).float()
         torch.testing.assert_close(k_rows, ref[:, D:2 * D], atol=2e-2, rtol=2e-2)
         torch.testing.assert_close(v_rows, ref[:, 2 * D:], atol=2e-2, rtol=2e-2)
-        assert ops.gemm_tile_count(128, 128) == 1
+        assert ops.gemm_tile_count(*tile) == 1
         return
     N = 3072
     a, w = _bf(M, K, seed=23), _bf(N, K, scale=0.05, seed=24)
@@ -125,7 +127,7 @@ def test_gemm_256_tiles_large_m(epi):
     if epi == "gelu_tanh":
         ref = torch.nn.functional.gelu(ref, approximate="tanh")
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
-    assert ops.gemm_tile_count(128, 128) == 1
+    assert ops.gemm_tile_count(*tile) == 1
 
 
 @pytest.mark.parametrize("tile", [20, 21, 22, 23, 24, 25])
