@@ -147,7 +147,8 @@ for task in "$@"; do
         sweep:*)
             IFS=';' read -ra sets <<< "${task#sweep:}"
             for envs in "${sets[@]}"; do
-                step 300 gpurun_out/sweep.log env ${envs//,/ } python -u bench.py --steps 5 --warmup 2 --latency-batches ""
+                ev=${envs//,/ }; if [ "$ev" = "default" ]; then ev=""; fi
+                step 300 gpurun_out/sweep.log env $ev python -u bench.py --steps 5 --warmup 2 --latency-batches ""
                 echo "{\"env\": \"$envs\", \"bench\": $(grep '^{' gpurun_out/sweep.log | tail -1)}" >> gpurun_out/sweep.jsonl
                 tail -1 gpurun_out/sweep.jsonl
             done ;;
