@@ -311,6 +311,25 @@ __device__ __forceinline__ void load_ln(const float* g, const float* b, float (&
     }
 }
 
+// d >= 1024 register diet of the comm wave (its arrays of D / 64 values per lane set the whole
+// kernel's allocation: 1280 / 1600 spilled 72 / 158 VGPRs): the bias is added into this CU's residual
+// copy BEFORE the poll (its load hides under the all-to-all wait) instead of being held through it,
+// and gamma / beta are loaded after the poll instead of across it
+template <int D>
+constexpr bool big_d() { return D >= 1024; }
+
+template <int D, int R>
+__device__ __forceinline__ void add_bias_xs(i64* xs, const float* bias, int lane) {
+    constexpr int EPL = D / 64;
+    float b[EPL];
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) b[i] = gl(bias + lane + 64 * i);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int i = 0; i < EPL; ++i) xs[r * D + lane + 64 * i] += f2fix(b[i]);
+}
+
 template <int D, int R>
 __device__ __forceinline__ void layer_norm(float (&x)[R][D / 64], const float (&gg)[D / 64], const float (&bb)[D / 64],
                                            float eps, bf16_t* xn_lds, int lane) {
@@ -514,7 +533,8 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
             // int64 fixed point): x += (sum of the previous MLP's contributions) + b_proj
             float xf[R][EPL];
             float gg[EPL], bb[EPL];
-            load_ln<D>(lw.ln1_g, lw.ln1_b, gg, bb, lane);  // issued before the wait: off the critical path
+            if constexpr (!big_d<D>())
+                load_ln<D>(lw.ln1_g, lw.ln1_b, gg, bb, lane);  // issued before the wait: off the critical path
             if (l == 0) {
 #pragma unroll
                 for (int r = 0; r < R; ++r)
@@ -526,12 +546,19 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
                     }
             } else {
                 float bp[EPL];
+                if constexpr (big_d<D>()) {
+                    add_bias_xs<D, R>(xs, a.layers[l - 1].b_p, lane);
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) bp[i] = gl(a.layers[l - 1].b_p + lane + 64 * i);
+                    for (int i = 0; i < EPL; ++i) bp[i] = 0.f;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < EPL; ++i) bp[i] = gl(a.layers[l - 1].b_p + lane + 64 * i);
+                }
                 if (!(ok = poll_resid<D, R>(sw + (2 * (l - 1) + 1) * sc.xw, a.exp_mlp, bp, xs, a, ctl, 10 * l + 1, s,
                                             lane)))
                     break;
             }
+            if constexpr (big_d<D>()) load_ln<D>(lw.ln1_g, lw.ln1_b, gg, bb, lane);
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -603,13 +630,20 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
                 stamp(a, s, l, 7, lane);
             }
             // ---------------- E3: XA complete -> LN2 -> MLP
-            load_ln<D>(lw.ln2_g, lw.ln2_b, gg, bb, lane);
+            if constexpr (!big_d<D>()) load_ln<D>(lw.ln2_g, lw.ln2_b, gg, bb, lane);
             {
                 float bo[EPL];
+                if constexpr (big_d<D>()) {
+                    add_bias_xs<D, R>(xs, lw.b_o, lane);
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) bo[i] = gl(lw.b_o + lane + 64 * i);
+                    for (int i = 0; i < EPL; ++i) bo[i] = 0.f;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < EPL; ++i) bo[i] = gl(lw.b_o + lane + 64 * i);
+                }
                 if (!(ok = poll_resid<D, R>(sw + (2 * l) * sc.xw, a.exp_att, bo, xs, a, ctl, 10 * l + 3, s, lane))) break;
             }
+            if constexpr (big_d<D>()) load_ln<D>(lw.ln2_g, lw.ln2_b, gg, bb, lane);
             stamp(a, s, l, 8, lane);
             stamp(a, s, l, 25, lane);
 #pragma unroll
@@ -638,11 +672,18 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
         {
             float xf[R][EPL];
             float gg[EPL], bb[EPL], bp[EPL];
-            load_ln<D>(a.lnf_g, a.lnf_b, gg, bb, lane);
+            if constexpr (big_d<D>()) {
+                add_bias_xs<D, R>(xs, a.layers[L - 1].b_p, lane);
 #pragma unroll
-            for (int i = 0; i < EPL; ++i) bp[i] = gl(a.layers[L - 1].b_p + lane + 64 * i);
+                for (int i = 0; i < EPL; ++i) bp[i] = 0.f;
+            } else {
+                load_ln<D>(a.lnf_g, a.lnf_b, gg, bb, lane);
+#pragma unroll
+                for (int i = 0; i < EPL; ++i) bp[i] = gl(a.layers[L - 1].b_p + lane + 64 * i);
+            }
             if (!(ok = poll_resid<D, R>(sw + (2 * (L - 1) + 1) * sc.xw, a.exp_mlp, bp, xs, a, ctl, 10 * L + 1, s, lane)))
                 break;
+            if constexpr (big_d<D>()) load_ln<D>(a.lnf_g, a.lnf_b, gg, bb, lane);
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
