@@ -808,8 +808,9 @@ __global__ __launch_bounds__(256) void skinny_mlp_kernel(
     }
 
     // (1) residual rows -> LN2 -> LDS image (block 0 also keeps v); (2) c_fc slice on MFMA
-    // (gamma / beta with the residual loads here: one workgroup per CU either way, so the register
-    // saving of a late load would buy no occupancy, only a round trip)
+    // (gamma / beta with the residual loads: a late load buys no occupancy at the default column
+    // groups, only a round trip; GPT-2-XL at one group per workgroup, where it does give two waves
+    // per SIMD, still ran 255 vs 217.5 ms per query at two groups, profiles/r4_xl_mlp_cg_ab.jsonl)
     addln_rows_lds<NSPLIT, NV4, RPW, XFIX, false>(x_in, nullptr, ldx, parts, ldp, split_stride, res_bias, gamma, beta, eps, M,
                                            K, smem, ROWB, xcs, blockIdx.x == 0 ? v_lds : nullptr, issue_wp);
     __syncthreads();
