@@ -127,7 +127,7 @@ struct Args {
     int fault_step;  // test hook: >= 0 makes the last CU abort at that step as a timed-out wait would
     int coop;        // launch cooperatively (co-residency guaranteed by the runtime)
     int gather_pause;  // loaders pause while the comm wave waits on a hand-off (C_GATHER)
-    int pad_args;
+    int spec_rem;      // residual poll: start reading whole rows once the watched word lacks <= this many adds
     int exp_att[8], exp_mlp[8];  // contributions each residual copy receives (attention / MLP CUs)
     float eps, penalty;
 };
@@ -369,7 +369,11 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
     if (a.gather_pause) lds_st(ctl + C_GATHER, 1u);
     const u64 t0 = clk();
     // phase 1: poll ONE word per copy -- the element every producer adds last (row R-1, element
-    // D-1) -- so 256 pollers do not hammer the lines the atomics are still updating
+    // D-1) -- so 256 pollers do not hammer the lines the atomics are still updating.  With
+    // spec_rem > 0 phase 2 (whole rows, exact counts checked per word) starts once that word lacks at
+    // most spec_rem adds: the last producers' adds then land under row reads already in flight,
+    // one round trip fewer per hand-off than watching the word reach its final count first
+    const int rem = a.spec_rem;
     for (;;) {
         bool done = true;
         if (lane < COPIES) {
@@ -377,7 +381,7 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
             int want = ec[0];
 #pragma unroll
             for (int c = 1; c < COPIES; ++c) want = lane == c ? ec[c] : want;
-            done = (int)(x[1] >> 24) == want;
+            done = (int)(x[1] >> 24) >= want - rem;
         }
         if (__all(done)) break;
         if ((unsigned)__builtin_amdgcn_readfirstlane((int)gld32(a.err)) || lds_ld(ctl + C_ABORT)) {

@@ -42,7 +42,7 @@ class DfLayer(ctypes.Structure):
 
 
 _INT_FIELDS = ("R", "D", "H", "L", "V", "T", "seen_words", "eos", "nsteps", "A", "C", "max_nq", "swl", "ring_bytes",
-               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop", "gather_pause", "pad_args")
+               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop", "gather_pause", "spec_rem")
 
 
 class DfArgs(ctypes.Structure):
@@ -397,6 +397,10 @@ class DataflowDecoder:
         a.fault_step, self._fault_step = self._fault_step, -1
         a.coop = int(self.coop)
         a.gather_pause = int(os.environ.get("DLMS_DF_GATHER_PAUSE", "1") != "0")
+        # residual poll: whole-row reads start this many adds before the watched word completes
+        # (0: only once it has): batch 1 28.8 -> 28.2 ms at 4 (1 / 2 / 8: 28.6 / 28.4 / 29.0),
+        # GPT-2-medium 66.7 -> 65.6 (profiles/r4_df_spec_poll_sweep.jsonl); A/B knob DLMS_DF_SPEC
+        a.spec_rem = int(os.environ.get("DLMS_DF_SPEC", "4"))
         for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
             a.exp_mlp[c] = self._exp_mlp[c]
             a.exp_att[c] = self._exp_att[c]
