@@ -128,6 +128,8 @@ struct Args {
     int coop;        // launch cooperatively (co-residency guaranteed by the runtime)
     int gather_pause;  // loaders pause while the comm wave waits on a hand-off (C_GATHER)
     int spec_rem;      // residual poll: start reading whole rows once the watched word lacks <= this many adds
+    int argmax_slots;  // per-step argmax: every CU stores its best key in a slot of its own, all CUs read all slots
+    int pad_args2;
     int exp_att[8], exp_mlp[8];  // contributions each residual copy receives (attention / MLP CUs)
     float eps, penalty;
 };
@@ -178,7 +180,7 @@ enum { E_WAIT_CNT = 1, E_WAIT_GRAN = 2, E_WAIT_LDS = 3, E_LOADER = 4, E_INJECTED
 
 // scratch word offsets (per step)
 struct Scr {
-    long long xw, qkv0, cnt0, keys, words;
+    long long xw, qkv0, cnt0, keys, kslots, words;
 };
 __host__ __device__ inline Scr scratch_layout(int R, int D, int L, int C) {
     Scr s;
@@ -187,7 +189,8 @@ __host__ __device__ inline Scr scratch_layout(int R, int D, int L, int C) {
     long long c = s.qkv0 + (long long)L * R * 3 * D;
     s.cnt0 = (c + 15) & ~15LL;
     s.keys = s.cnt0 + (2LL * L + 1) * SHARDS * CSTRIDE;
-    s.words = s.keys + 16 + ((R + 15) & ~15);
+    s.kslots = s.keys + 16 + ((R + 15) & ~15);  // [R][256] per-CU best keys (argmax_slots)
+    s.words = s.kslots + 256LL * R;
     return s;
 }
 
@@ -317,6 +320,14 @@ __device__ __forceinline__ void load_ln(const float* g, const float* b, float (&
 // and gamma / beta are loaded after the poll instead of across it
 template <int D>
 constexpr bool big_d() { return D >= 1024; }
+// the residual poll hands the updated row back as floats (the LayerNorm's input) instead of a second
+// LDS pass over it: one row at d 768, 28.5-28.6 -> 28.2 ms per query; at d 1024 it took the kernel
+// to 246 VGPRs and GPT-2-medium from 65.8 to 68.0 ms (profiles/r4_df_xf_slots_ab.jsonl), so not there
+#ifndef DF_XF_POLL
+#define DF_XF_POLL 1  // A/B build knob (-DDF_XF_POLL=0: LayerNorm input re-read from LDS)
+#endif
+template <int D, int R>
+constexpr bool xf_from_poll() { return DF_XF_POLL && R == 1 && D <= 768; }
 
 template <int D, int R>
 __device__ __forceinline__ void add_bias_xs(i64* xs, const float* bias, int lane) {
@@ -354,12 +365,12 @@ __device__ __forceinline__ void layer_norm(float (&x)[R][D / 64], const float (&
 
 // Poll residual-update buffer X (COPIES x R rows x D counted words, sc1 buffer loads) until every
 // word carries exactly expc[copy] contributions, then add the exact integer sum of the copies (+
-// the bias) to this CU's own copy of the residual xs.  The buffer is fresh per step, so a word can
+// the bias) to this CU's own copy of the residual xs (and hand the new row back as floats in xf).  The buffer is fresh per step, so a word can
 // only ever read below its final count.
 template <int D, int R>
 __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const float (&bias)[D / 64],
-                                           i64* xs, const Args& a, unsigned* ctl, unsigned where, int s,
-                                           int lane) {
+                                           i64* xs, float (&xf)[R][D / 64], const Args& a, unsigned* ctl,
+                                           unsigned where, int s, int lane) {
     constexpr int EPL = D / 64;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, COPIES * R * D * 8, 0x00020000);
@@ -424,7 +435,9 @@ __device__ __forceinline__ bool poll_resid(const u64* X, const int* expc, const 
                     i64 t = f2fix(bias[i]);
 #pragma unroll
                     for (int c = 0; c < COPIES; ++c) t += (i64)(v[c][i] & CNT_MASK) - (i64)ec[c] * CNT_BIAS;
-                    xs[r * D + lane + 64 * i] += t;
+                    const i64 nx = xs[r * D + lane + 64 * i] + t;
+                    xs[r * D + lane + 64 * i] = nx;
+                    if constexpr (xf_from_poll<D, R>()) xf[r][i] = fix2f(nx);
                 }
                 pending &= ~(1u << r);
             }
@@ -545,8 +558,10 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
 #pragma unroll
                     for (int i = 0; i < EPL; ++i) {
                         const int e = lane + 64 * i;
-                        xs[r * D + e] = f2fix(bf16_to_f32(a.wte[(size_t)tok[r] * D + e]) +
-                                         bf16_to_f32(a.wpe[(size_t)pos[r] * D + e]));
+                        const i64 x0 = f2fix(bf16_to_f32(a.wte[(size_t)tok[r] * D + e]) +
+                                             bf16_to_f32(a.wpe[(size_t)pos[r] * D + e]));
+                        xs[r * D + e] = x0;
+                        if constexpr (xf_from_poll<D, R>()) xf[r][i] = fix2f(x0);
                     }
             } else {
                 float bp[EPL];
@@ -558,15 +573,17 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
 #pragma unroll
                     for (int i = 0; i < EPL; ++i) bp[i] = gl(a.layers[l - 1].b_p + lane + 64 * i);
                 }
-                if (!(ok = poll_resid<D, R>(sw + (2 * (l - 1) + 1) * sc.xw, a.exp_mlp, bp, xs, a, ctl, 10 * l + 1, s,
-                                            lane)))
+                if (!(ok = poll_resid<D, R>(sw + (2 * (l - 1) + 1) * sc.xw, a.exp_mlp, bp, xs, xf, a, ctl, 10 * l + 1,
+                                            s, lane)))
                     break;
             }
             if constexpr (big_d<D>()) load_ln<D>(lw.ln1_g, lw.ln1_b, gg, bb, lane);
+            if constexpr (!xf_from_poll<D, R>()) {
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+                for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
+                    for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
+            }
             stamp(a, s, l, 1, lane);
             layer_norm<D, R>(xf, gg, bb, a.eps, xn, lane);
             unsigned pid = pid_of(s, l, 0, L);
@@ -645,15 +662,18 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
 #pragma unroll
                     for (int i = 0; i < EPL; ++i) bo[i] = gl(lw.b_o + lane + 64 * i);
                 }
-                if (!(ok = poll_resid<D, R>(sw + (2 * l) * sc.xw, a.exp_att, bo, xs, a, ctl, 10 * l + 3, s, lane))) break;
+                if (!(ok = poll_resid<D, R>(sw + (2 * l) * sc.xw, a.exp_att, bo, xs, xf, a, ctl, 10 * l + 3, s, lane)))
+                    break;
             }
             if constexpr (big_d<D>()) load_ln<D>(lw.ln2_g, lw.ln2_b, gg, bb, lane);
             stamp(a, s, l, 8, lane);
             stamp(a, s, l, 25, lane);
+            if constexpr (!xf_from_poll<D, R>()) {
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+                for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
+                    for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
+            }
             layer_norm<D, R>(xf, gg, bb, a.eps, xn, lane);
             pid = pid_of(s, l, 2, L);
             lds_st(ctl + C_READY, pid);
@@ -685,13 +705,16 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
 #pragma unroll
                 for (int i = 0; i < EPL; ++i) bp[i] = gl(a.layers[L - 1].b_p + lane + 64 * i);
             }
-            if (!(ok = poll_resid<D, R>(sw + (2 * (L - 1) + 1) * sc.xw, a.exp_mlp, bp, xs, a, ctl, 10 * L + 1, s, lane)))
+            if (!(ok = poll_resid<D, R>(sw + (2 * (L - 1) + 1) * sc.xw, a.exp_mlp, bp, xs, xf, a, ctl, 10 * L + 1, s,
+                                        lane)))
                 break;
             if constexpr (big_d<D>()) load_ln<D>(a.lnf_g, a.lnf_b, gg, bb, lane);
+            if constexpr (!xf_from_poll<D, R>()) {
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+                for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
+                    for (int i = 0; i < EPL; ++i) xf[r][i] = fix2f(xs[r * D + lane + 64 * i]);
+            }
             stamp(a, s, L, 0, lane);
             stamp_val(a, s, L, 26, __builtin_amdgcn_s_memtime());
             stamp_val(a, s, L, 27, wall_clock64());
@@ -702,32 +725,97 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
         stamp(a, s, L, 1, lane);
         if (!(ok = wait_phdone(ctl, pid, a, s))) break;
         stamp(a, s, L, 2, lane);
-        if (lane < R) {
-            u64 best = 0;
+        u64 best_all[R];
+        if (a.argmax_slots) {
+            // this CU's best key per row into a slot of its own, repacked as (ordered value : 32,
+            // 65535 - token : 16, 1 : 16) -- the same order, never zero -- then every CU reads all G
+            // slots of the (fresh per step) scratch until none is zero: one store and one polling
+            // round trip, instead of an atomic max, its drain, a counter add and the counter poll
+            // followed by a separate read of the result
+            if (lane < R) {
+                u64 best = 0;
 #pragma unroll
-            for (int w = 0; w < NC; ++w) {
-                const u64 k = keys[w * R + lane];
-                best = k > best ? k : best;
+                for (int w = 0; w < NC; ++w) {
+                    const u64 k = keys[w * R + lane];
+                    best = k > best ? k : best;
+                }
+                const u64 packed = best ? ((best >> 32) << 32) |
+                                              ((u64)(0xffffu - ((~(unsigned)(best & 0xffffffffull)) & 0xffffu)) << 16) | 1ull
+                                        : 1ull;
+                gst64(sw + sc.kslots + (size_t)lane * 256 + blockIdx.x, packed);
             }
-            if (best) __hip_atomic_fetch_max(sw + sc.keys + lane, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stamp(a, s, L, 3, lane);
+            const u64 t0 = clk();
+            for (;;) {
+                bool all = true;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    u64 m = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {  // G <= 256 slots over 64 lanes
+                        const int c = lane + 64 * j;
+                        const u64 k = c < G ? gld64(sw + sc.kslots + (size_t)r * 256 + c) : 1ull;
+                        all &= k != 0ull;
+                        m = k > m ? k : m;
+                    }
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)m, o);
+                        const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(m >> 32), o);
+                        const u64 k = ((u64)hi << 32) | lo;
+                        m = k > m ? k : m;
+                    }
+                    best_all[r] = m;
+                }
+                if (__all(all)) break;
+                if ((unsigned)__builtin_amdgcn_readfirstlane((int)gld32(a.err)) || lds_ld(ctl + C_ABORT)) {
+                    lds_st(ctl + C_ABORT, 1u);
+                    ok = false;
+                    break;
+                }
+                if (clk() - t0 > TIMEOUT_TICKS) {
+                    set_err(a, E_WAIT_CNT, 10 * L + 2, s);
+                    lds_st(ctl + C_ABORT, 1u);
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) break;
+        } else {
+            if (lane < R) {
+                u64 best = 0;
+#pragma unroll
+                for (int w = 0; w < NC; ++w) {
+                    const u64 k = keys[w * R + lane];
+                    best = k > best ? k : best;
+                }
+                if (best) __hip_atomic_fetch_max(sw + sc.keys + lane, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            drain();
+            if (lane == 0) gadd64(sw + sc.cnt0 + (2 * L) * SHARDS * CSTRIDE + shard * CSTRIDE, 1ull);
+            stamp(a, s, L, 3, lane);
+            if (!(ok = wait_count(sw + sc.cnt0 + (2 * L) * SHARDS * CSTRIDE, (u64)G, a, ctl, 10 * L + 2, s, lane))) break;
+#pragma unroll
+            for (int r = 0; r < R; ++r) best_all[r] = gld64(sw + sc.keys + r);
         }
-        drain();
-        if (lane == 0) gadd64(sw + sc.cnt0 + (2 * L) * SHARDS * CSTRIDE + shard * CSTRIDE, 1ull);
-        stamp(a, s, L, 3, lane);
-        if (!(ok = wait_count(sw + sc.cnt0 + (2 * L) * SHARDS * CSTRIDE, (u64)G, a, ctl, 10 * L + 2, s, lane))) break;
         stamp(a, s, L, 4, lane);
         // ---------------- greedy bookkeeping (decode_update's semantics, replicated in every CU)
         bool any_live = false;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const u64 best = gld64(sw + sc.keys + r);
+            const u64 best = best_all[r];
             const int len0 = len[r];
             const int fin0 = fin[r];
             const int live_len = fin0 ? 0 : len0;
             int p = fin0 ? len0 - 1 : live_len;
             p = p < 0 ? 0 : (p < T - 1 ? p : T - 1);
             if (!fin0) {
-                int t = best ? (int)(~(unsigned)(best & 0xffffffffull)) : a.eos;
+                int t;
+                if (a.argmax_slots)  // (value : 32, 65535 - token : 16, 1 : 16); 1 = no candidate anywhere
+                    t = (best >> 16) ? (int)(0xffffu - (unsigned)((best >> 16) & 0xffffull)) : a.eos;
+                else
+                    t = best ? (int)(~(unsigned)(best & 0xffffffffull)) : a.eos;
                 t = (t >= 0 && t < a.V) ? t : a.eos;
                 if (blockIdx.x == 0 && lane == 0) a.out_tokens[(size_t)slot[r] * T + live_len] = t;
                 // (this CU's LDS slice only: the global bitmap is updated at the commit, so an

@@ -42,7 +42,7 @@ class DfLayer(ctypes.Structure):
 
 
 _INT_FIELDS = ("R", "D", "H", "L", "V", "T", "seen_words", "eos", "nsteps", "A", "C", "max_nq", "swl", "ring_bytes",
-               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop", "gather_pause", "spec_rem")
+               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop", "gather_pause", "spec_rem", "argmax_slots", "pad_args2")
 
 
 class DfArgs(ctypes.Structure):
@@ -401,6 +401,11 @@ class DataflowDecoder:
         # (0: only once it has): batch 1 28.8 -> 28.2 ms at 4 (1 / 2 / 8: 28.6 / 28.4 / 29.0),
         # GPT-2-medium 66.7 -> 65.6 (profiles/r4_df_spec_poll_sweep.jsonl); A/B knob DLMS_DF_SPEC
         a.spec_rem = int(os.environ.get("DLMS_DF_SPEC", "4"))
+        # per-step argmax hand-off through one slot per CU instead of an atomic max + arrival counter
+        # (two round trips fewer per token): 28.2 -> 27.9 ms per query, GPT-2-medium -0.25 ms
+        # (profiles/r4_df_xf_slots_ab.jsonl); DLMS_DF_ARGMAX_SLOTS=0 for the counter (A/B)
+        a.argmax_slots = int(os.environ.get("DLMS_DF_ARGMAX_SLOTS", "1") != "0" and self.eng.cfg.vocab_size <= 65535
+                             and self.G <= 256)
         for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
             a.exp_mlp[c] = self._exp_mlp[c]
             a.exp_att[c] = self._exp_att[c]
