@@ -91,7 +91,7 @@ struct Cu {           // per-CU assignment (host-built table, ops/dataflow.py as
     int ak0, akn;     // ... over the head dims [ak0, ak0 + akn)
     int pd0, pdn;     // c_proj output columns [pd0, pd0 + pdn) of the slice
     int acp, mcp;     // residual copy of the attention / MLP contributions
-    int pad;
+    int lm_off;       // byte offset of its LM-head rows within one step's stream (after the L layers)
     long long off;    // byte offset of this CU's packed row stream
     long long step_bytes;
 };
@@ -886,7 +886,7 @@ __device__ __forceinline__ void comm_wave(const Args& a, const Cu& cu, char* lds
 // far more in flight.)
 constexpr int LB = 8;  // units per batch (the ring is a multiple of LB KiB)
 constexpr unsigned BATCH = LB * 1024u;
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void loader_wave(const Args& a, const Cu& cu, char* lds, const Lay& ly, int j, int lane) {
     unsigned* ctl = reinterpret_cast<unsigned*>(lds + ly.ctl);
     const unsigned RB = (unsigned)a.ring_bytes;
@@ -925,13 +925,20 @@ __device__ __forceinline__ void loader_wave(const Args& a, const Cu& cu, char* l
         t0 = clk();
         unsigned gpos = (b * BATCH) % SB;
         unsigned rpos = (b * BATCH) % RB;
+        // NT 1: every weight byte non-temporal; NT 2: the layers' bytes only, the LM-head rows (the
+        // batch's start decides, a wave-uniform branch: one load per unit, the counted waits hold)
+        // keep the default policy, so they may stay in the Infinity Cache from one token to the next
+        const bool nt_here = NT == 1 || (NT == 2 && gpos < (unsigned)cu.lm_off);
 #pragma unroll
         for (int u = 0; u < LB; ++u) {
             unsigned lo = gpos + (unsigned)lane * 16u;
             if (lo >= SB) lo -= SB;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + lo),
-                                             (__attribute__((address_space(3))) void*)(ring + rpos), 16, 0,
-                                             NT ? 2 : 0);
+            if (nt_here)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + lo),
+                                                 (__attribute__((address_space(3))) void*)(ring + rpos), 16, 0, 2);
+            else
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + lo),
+                                                 (__attribute__((address_space(3))) void*)(ring + rpos), 16, 0, 0);
             gpos += 1024u;
             if (gpos >= SB) gpos -= SB;
             rpos += 1024u;
@@ -1469,10 +1476,12 @@ __global__ __launch_bounds__(NTHREADS, 1) void dataflow_decode_kernel(Args a) {
     if (wave == 0) {
         comm_wave<D, R>(a, cu, smem, ly, lane);
     } else if (wave <= NL) {
-        if (a.nt_weights)
-            loader_wave<true>(a, cu, smem, ly, wave - 1, lane);
+        if (a.nt_weights == 1)
+            loader_wave<1>(a, cu, smem, ly, wave - 1, lane);
+        else if (a.nt_weights == 2)
+            loader_wave<2>(a, cu, smem, ly, wave - 1, lane);
         else
-            loader_wave<false>(a, cu, smem, ly, wave - 1, lane);
+            loader_wave<0>(a, cu, smem, ly, wave - 1, lane);
     } else {
         compute_wave<D, R, PFG>(a, cu, smem, ly, wave - 1 - NL, lane);
     }

@@ -32,7 +32,7 @@ P = ctypes.c_void_p
 
 class DfCu(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("q0", "nq", "f0", "nf", "v0", "nv", "ah", "ao0", "aon", "ak0", "akn",
-                                            "pd0", "pdn", "acp", "mcp", "pad")] + \
+                                            "pd0", "pdn", "acp", "mcp", "lm_off")] + \
                [("off", ctypes.c_longlong), ("step_bytes", ctypes.c_longlong)]
 
 
@@ -290,7 +290,7 @@ class DataflowDecoder:
         tab = (DfCu * G)()
         for c, cu in enumerate(self.cus):
             tab[c] = DfCu(cu.q0, cu.nq, cu.f0, cu.nf, cu.v0, cu.nv, cu.ah, cu.ao0, cu.aon, cu.ak0, cu.akn, cu.pd0,
-                          cu.pdn, cu.acp, cu.mcp, 0, starts[c] * 2,
+                          cu.pdn, cu.acp, cu.mcp, cfg.n_layer * cu.layer_elems(D, self.ko, self.kf) * 2, starts[c] * 2,
                           cu.step_elems(cfg.n_layer, D, self.ko, self.kf) * 2)
         self.max_step_bytes = max(cu.step_elems(cfg.n_layer, D, self.ko, self.kf) for cu in self.cus) * 2
         self.cu_tab = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
@@ -392,7 +392,11 @@ class DataflowDecoder:
         a.nsteps, a.A, a.C, a.max_nq, a.swl = nsteps, self.A, self.COPIES, self.max_nq, self.swl
         a.ring_bytes, a.ldx, a.n_slots, a.P = self.ring_bytes(B), eng.x.stride(0), eng.max_batch, cfg.n_positions
         a.eps, a.penalty = cfg.layer_norm_epsilon, float(penalty)
-        a.nt_weights = int(os.environ.get("DLMS_DF_NT", "0") == "1")
+        # weight-stream cache policy: 0 default, 1 non-temporal, 2 non-temporal for the layers only.
+        # Non-temporal at d 768: 28.1 -> 27.6-27.7 ms per query (1 and 2 alike); GPT-2-medium 66.5 ->
+        # 66.8 with 2, so default policy there (profiles/r4_df_nt_ab.jsonl)
+        nt = os.environ.get("DLMS_DF_NT", "1" if cfg.n_embd <= 768 else "0")
+        a.nt_weights = int(nt) if nt in ("0", "1", "2") else 0
         a.ko, a.kf = self.ko, self.kf
         a.fault_step, self._fault_step = self._fault_step, -1
         a.coop = int(self.coop)
