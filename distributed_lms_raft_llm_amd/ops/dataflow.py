@@ -393,9 +393,9 @@ class DataflowDecoder:
         a.ring_bytes, a.ldx, a.n_slots, a.P = self.ring_bytes(B), eng.x.stride(0), eng.max_batch, cfg.n_positions
         a.eps, a.penalty = cfg.layer_norm_epsilon, float(penalty)
         # weight-stream cache policy: 0 default, 1 non-temporal, 2 non-temporal for the layers only.
-        # Non-temporal at d 768: 28.1 -> 27.6-27.7 ms per query (1 and 2 alike); GPT-2-medium 66.5 ->
-        # 66.8 with 2, so default policy there (profiles/r4_df_nt_ab.jsonl)
-        nt = os.environ.get("DLMS_DF_NT", "1" if cfg.n_embd <= 768 else "0")
+        # Non-temporal: batch 1 28.1 -> 27.6-27.7 ms per query (1 and 2 alike), GPT-2-medium 66.5 ->
+        # 65.7-66.0 with 1 (66.8 with 2) (profiles/r4_df_nt_ab.jsonl)
+        nt = os.environ.get("DLMS_DF_NT", "1")
         a.nt_weights = int(nt) if nt in ("0", "1", "2") else 0
         a.ko, a.kf = self.ko, self.kf
         a.fault_step, self._fault_step = self._fault_step, -1
