@@ -5,6 +5,8 @@
 // Query row r attends keys [0, row_kvlen[r]) of slot row_slot[r]: causal GPT-2 decode/prefill passes
 // kvlen = pos + 1, the bidirectional BERT encoder passes kvlen = sequence length.
 // Scores for the whole row live in LDS (t_max <= 2048), so the softmax is an exact two-pass one.
+#include <stdlib.h>
+
 #include "common.h"
 
 #define ATT_MAX_T 2048
@@ -207,7 +209,11 @@ __global__ __launch_bounds__(256) void attn_wave_kernel(const bf16_t* __restrict
 // so ~8 waves per CU still stream HBM at full rate -- and leave the CU's other wave slots, LDS and
 // MFMA pipes to the GEMMs of the other row half running on the second stream (a one-wave-per-pair
 // grid of 6k waves occupies every slot and serialises the two streams at kernel granularity).
-template <int U>
+//
+// BLK: the online softmax rescales once per block of U keys (one max, one correction exp2 and one
+// acc*corr pass per block instead of per key), halving the exp2 count and dropping 8 multiplies per
+// key from the VALU stream that shares the CU with the other stream's GEMMs.
+template <int U, bool BLK>
 __global__ __launch_bounds__(256) void attn_persist_kernel(const bf16_t* __restrict__ q, int ldq,
                                                            const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                                            const int* __restrict__ row_slot,
@@ -242,6 +248,40 @@ __global__ __launch_bounds__(256) void attn_persist_kernel(const bf16_t* __restr
                 const u32x4_t b = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(V + (size_t)t * 64));
                 kr[u] = make_uint4(a.x, a.y, a.z, a.w);
                 vr[u] = make_uint4(b.x, b.y, b.z, b.w);
+            }
+            if constexpr (BLK) {
+                float sv[U];
+                float mb = -INFINITY;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    float kf[8];
+                    unpack8(kr[u], kf);
+                    float s = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) s += qf[j] * kf[j];
+                    s = group8_sum(s);
+                    sv[u] = t0 + u * 8 + g < kvlen ? s : -INFINITY;
+                    mb = fmaxf(mb, sv[u]);
+                }
+                if (mb != -INFINITY) {  // else every key of this lane group is past kvlen
+                    const float m_new = fmaxf(m, mb);
+                    const float corr = exp2f(m - m_new);  // m == -inf -> 0
+                    float ps = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[j] *= corr;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const float p = exp2f(sv[u] - m_new);  // masked keys -> 0
+                        float vf[8];
+                        unpack8(vr[u], vf);
+                        ps += p;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc[j] += p * vf[j];
+                    }
+                    l = l * corr + ps;
+                    m = m_new;
+                }
+                continue;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -297,10 +337,21 @@ extern "C" hipError_t dlms_attention_persist(const void* q, int ldq, const void*
                                              hipStream_t stream) {
     if (R <= 0 || H <= 0 || t_max <= 0 || blocks <= 0) return hipErrorInvalidValue;
     const int need = (R * H + 3) / 4;
-    hipLaunchKernelGGL(attn_persist_kernel<8>, dim3(blocks < need ? blocks : need), dim3(256), 0, stream,
-                       reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
-                       reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, reinterpret_cast<bf16_t*>(out), ldo,
-                       R, H, t_max, n_slots, scale * 1.4426950408889634f);
+    static int blk = -1;  // DLMS_ATTN_BLK=0 restores the per-key softmax update
+    if (blk < 0) {
+        const char* e = getenv("DLMS_ATTN_BLK");
+        blk = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(blocks < need ? blocks : need), dim3(256), 0, stream,
+                           reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
+                           reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, reinterpret_cast<bf16_t*>(out),
+                           ldo, R, H, t_max, n_slots, scale * 1.4426950408889634f);
+    };
+    if (blk)
+        launch(attn_persist_kernel<8, true>);
+    else
+        launch(attn_persist_kernel<8, false>);
     return hipGetLastError();
 }
 

@@ -259,7 +259,7 @@ def test_layernorm(M, D):
     torch.testing.assert_close(ob.float(), ref, atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("impl", ["wave", "lds"])
+@pytest.mark.parametrize("impl", ["wave", "lds", "persist"])
 @pytest.mark.parametrize("kvlens", [[1, 5, 150], [64, 63, 65, 1024], [31, 33, 7, 2]])
 def test_row_attention(kvlens, impl):
     ops = _ops()
