@@ -86,13 +86,18 @@ def test_follower_down_through_100mib_snapshot_catches_up(tmp_path):
         lid = c.wait_leader()
         down = next(i for i in c.servers if i != lid)
         c.stop(down)
-        stub = c.stub(lid)
         blobs = {}
         for k in range(3):  # 3 x 36 MiB = 108 MiB while the follower is down
-            tok = _login(stub, f"s{k}", "student")
             data = os.urandom(36 << 20)
-            assert stub.Post(pb.PostRequest(token=tok, type="assignment", file=data, filename=f"a{k}.pdf"),
-                             timeout=120).success
+            for _attempt in range(3):  # a client retries at the current leader (a CPU-starved host can cost a term)
+                lid = c.wait_leader()
+                stub = c.stub(lid)
+                tok = _login(stub, f"s{k}_{_attempt}", "student")
+                ok = stub.Post(pb.PostRequest(token=tok, type="assignment", file=data, filename=f"a{k}.pdf"),
+                               timeout=120).success
+                if ok:
+                    break
+            assert ok, f"upload a{k} failed three times"
             blobs[f"uploads/a{k}.pdf"] = hashlib.sha256(data).hexdigest()
             del data
         leader = c.servers[lid]
