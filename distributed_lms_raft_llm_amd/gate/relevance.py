@@ -41,6 +41,9 @@ class RelevanceGate:
         self._cache: OrderedDict[str, torch.Tensor] = OrderedDict()
         self._cache_size = cache_size
         self._lock = threading.Lock()  # one encoder pass at a time (GPU stream / CPU threads)
+        # the embedding cache has its own lock, never held across encoder work: the aio front end
+        # reads it on the event-loop thread while the batcher may be inside a long encoder pass
+        self._cache_lock = threading.Lock()
         self.device = getattr(encoder, "device", torch.device("cpu"))
         # query batching: concurrent GetLLMAnswer calls share one packed encoder pass
         self.window_s = window_ms / 1e3
@@ -89,17 +92,22 @@ class RelevanceGate:
 
     def _cached(self, text: str) -> torch.Tensor:
         k = self._key(text)
-        with self._lock:
-            v = self._cache.get(k)
-            if v is not None:
-                self._cache.move_to_end(k)
-                return v
+        v = self._cache_get(k)
+        if v is not None:
+            return v
         v = self.embed([text])[0]
-        with self._lock:
+        with self._cache_lock:
             self._cache[k] = v
             if len(self._cache) > self._cache_size:
                 self._cache.popitem(last=False)
         return v
+
+    def _cache_get(self, k: str) -> torch.Tensor | None:
+        with self._cache_lock:
+            v = self._cache.get(k)
+            if v is not None:
+                self._cache.move_to_end(k)
+            return v
 
     def warm(self, text: str):
         self._cached(text)
@@ -176,9 +184,7 @@ class RelevanceGate:
         import asyncio
 
         loop = asyncio.get_running_loop()
-        k = self._key(assignment_text)
-        with self._lock:
-            a = self._cache.get(k)
+        a = self._cache_get(self._key(assignment_text))  # never waits on an encoder pass
         if a is None:
             a = await loop.run_in_executor(None, self._cached, assignment_text)
         s = float(await asyncio.wrap_future(self._submit(query, a)))

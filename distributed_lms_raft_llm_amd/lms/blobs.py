@@ -60,6 +60,7 @@ class BlobStore:
         os.makedirs(os.path.join(root, UPLOAD_FOLDER), exist_ok=True)
         os.makedirs(os.path.join(root, CAS_FOLDER), exist_ok=True)
         self.fetcher = None  # BlobFetcher: pulls objects this replica is missing
+        self._gc_lock = threading.Lock()  # _touch vs the GC's last re-check + unlink
 
     # ---------------------------------------------------------------- uploads/ (reference layout)
     def relpath(self, filename: str) -> str:
@@ -143,11 +144,12 @@ class BlobStore:
         already here counts as a fresh upload for the GC's grace period -- otherwise a stale
         unreferenced object re-uploaded just before a GC pass could be deleted under a PutBlob
         that is about to commit a reference to it."""
-        try:
-            os.utime(self.cas_path(sha))
-            return True
-        except FileNotFoundError:
-            return False
+        with self._gc_lock:  # never between the GC's last mtime check and its unlink
+            try:
+                os.utime(self.cas_path(sha))
+                return True
+            except FileNotFoundError:
+                return False
 
     def get_sha(self, sha: str, relpath: str | None = None, fetch_timeout: float = 30.0) -> bytes:
         """Bytes of CAS object ``sha`` (an entry's own upload: two same-named uploads keep their
@@ -163,31 +165,44 @@ class BlobStore:
                         break
         return self.get(relpath, sha) if relpath else b""
 
-    def gc(self, referenced: set[str], grace_s: float = 600.0, still_referenced=None) -> int:
+    def gc(self, referenced: set[str], grace_s: float = 600.0, live_refs=None) -> int:
         """Delete CAS objects no replicated entry references any more (snapshot time).  Objects
         younger than ``grace_s`` survive: a pre-replicated upload whose PutBlob has not committed
-        yet is unreferenced but live (re-uploads refresh the mtime, ``_touch``).  Each candidate
-        is re-checked right before its unlink -- its mtime read again, and ``still_referenced(sha)``
-        (the live state, not the snapshot-time set) asked -- since the scan runs in the
-        background while entries keep committing.  ``uploads/<name>`` links keep their own inode.
+        yet is unreferenced but live (re-uploads refresh the mtime, ``_touch``).  The scan runs in
+        the background while entries keep committing, so the candidates are re-checked against
+        ``live_refs()`` (the live state's reference set, built ONCE per pass, not per candidate)
+        and each one's mtime is read again right before its unlink -- that re-check and the unlink
+        hold ``_gc_lock``, which ``_touch`` holds too, so a re-upload either lands before the
+        re-check (the object survives) or after the unlink (``_touch`` sees it absent and the
+        upload writes it again).  ``uploads/<name>`` links keep their own inode.
         Returns the number of objects removed."""
         d = os.path.join(self.root, CAS_FOLDER)
-        removed = 0
+        now = time.time()
+        cands = []
         for name in os.listdir(d):
             if not is_sha256(name) or name in referenced:
                 continue
-            path = os.path.join(d, name)
             try:
-                if time.time() - os.path.getmtime(path) < grace_s:
-                    continue
-                if still_referenced is not None and still_referenced(name):
-                    continue
-                if time.time() - os.path.getmtime(path) < grace_s:  # touched meanwhile
-                    continue
-                os.unlink(path)
-                removed += 1
+                if now - os.path.getmtime(os.path.join(d, name)) >= grace_s:
+                    cands.append(name)
             except FileNotFoundError:
                 pass
+        if not cands:
+            return 0
+        live = live_refs() if live_refs is not None else set()
+        removed = 0
+        for name in cands:
+            if name in live:
+                continue
+            path = os.path.join(d, name)
+            with self._gc_lock:
+                try:
+                    if time.time() - os.path.getmtime(path) < grace_s:  # touched meanwhile
+                        continue
+                    os.unlink(path)
+                    removed += 1
+                except FileNotFoundError:
+                    pass
         return removed
 
     def _fsync_dir(self, path: str):

@@ -108,7 +108,7 @@ class LMSState:
 
     def _gc(self, refs: set[str]):
         try:
-            n = self.blobs.gc(refs, self.gc_grace_s, still_referenced=lambda sha: sha in self.referenced_blobs())
+            n = self.blobs.gc(refs, self.gc_grace_s, live_refs=self.referenced_blobs)
             if n:
                 log.info("blob gc: removed %d unreferenced object(s)", n)
         except OSError as e:

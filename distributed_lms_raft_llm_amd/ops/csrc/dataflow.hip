@@ -125,7 +125,7 @@ struct Args {
     int R, D, H, L, V, T, seen_words, eos, nsteps, A, C, max_nq, swl, ring_bytes, ldx, n_slots, P, nt_weights;
     int ko, kf;  // K (padded to 16) of the per-CU W_o block and c_proj block
     int fault_step;  // test hook: >= 0 makes the last CU abort at that step as a timed-out wait would
-    int coop;        // launch cooperatively (co-residency guaranteed by the runtime)
+    int pad_args1;
     int gather_pause;  // loaders pause while the comm wave waits on a hand-off (C_GATHER)
     int spec_rem;      // residual poll: start reading whole rows once the watched word lacks <= this many adds
     int argmax_slots;  // per-step argmax: every CU stores its best key in a slot of its own, all CUs read all slots
@@ -1501,33 +1501,35 @@ extern "C" int dlms_df_copies() { return df::COPIES; }
 
 // Every workgroup spins on the others, so the whole grid must be resident at once.  The launcher
 // checks that the device can hold it (occupancy x CUs >= grid; -2 = "cannot", the host then serves
-// the launch-per-op path) and by default launches cooperatively, which makes the runtime guarantee
-// co-residency against other work on the device as well; the bounded waits + commit-only row
-// state are the last line (an aborted launch changes nothing the next launch reads).
+// the launch-per-op path); the bounded waits + commit-only row state are the last line (an aborted
+// launch changes nothing the next launch reads).  A plain launch: hipLaunchCooperativeKernel gives
+// the same residency (MI355X_MICROARCH.md "coop-launch") and reserves nothing against other
+// processes either, but measured +1.1 ms per query behind a 1024-query generation on the same
+// engine -- its queue hand-over held the preceding prefill's completion (prefill 0.7 -> 1.8 ms,
+// profiles/r5_prefill_b1_coop_probe.jsonl).
 constexpr int DF_NOT_RESIDENT = -2;
+constexpr int DF_MAX_DEVICES = 64;
 template <int D, int R, int PFG>
 static int df_launch(df::Args a, int grid, int lds, hipStream_t stream) {
     auto k = &df::dataflow_decode_kernel<D, R, PFG>;
-    static int fits_grid = -1;  // the most workgroups the device holds at once (per instantiation)
-    if (fits_grid < 0) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           df::LDS_MAX);
-        if (e != hipSuccess) return (int)e;
-        int dev = 0, cus = 0, per_cu = 0;
-        if ((e = hipGetDevice(&dev)) != hipSuccess) return (int)e;
+    static int fits_grid[DF_MAX_DEVICES];  // per device: the most workgroups it holds at once (0: not queried)
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    if (dev < 0 || dev >= DF_MAX_DEVICES) return (int)hipErrorInvalidDevice;
+    if (fits_grid[dev] <= 0) {
+        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     df::LDS_MAX)) != hipSuccess)
+            return (int)e;
+        int cus = 0, per_cu = 0;
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return (int)e;
         // (occupancy at the largest LDS any launch of this instantiation asks for)
         if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k), df::NTHREADS,
                                                               df::LDS_MAX)) != hipSuccess)
             return (int)e;
-        fits_grid = per_cu * cus;
+        fits_grid[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
     }
-    if (grid > fits_grid) return DF_NOT_RESIDENT;
-    if (a.coop) {
-        void* params[] = {&a};
-        return (int)hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k), dim3(grid), dim3(df::NTHREADS), params,
-                                               (unsigned)lds, stream);
-    }
+    if (grid > fits_grid[dev]) return DF_NOT_RESIDENT;
     hipLaunchKernelGGL(k, dim3(grid), dim3(df::NTHREADS), lds, stream, a);
     return (int)hipGetLastError();
 }

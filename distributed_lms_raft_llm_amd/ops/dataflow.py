@@ -42,7 +42,7 @@ class DfLayer(ctypes.Structure):
 
 
 _INT_FIELDS = ("R", "D", "H", "L", "V", "T", "seen_words", "eos", "nsteps", "A", "C", "max_nq", "swl", "ring_bytes",
-               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "coop", "gather_pause", "spec_rem", "argmax_slots", "pad_args2")
+               "ldx", "n_slots", "P", "nt_weights", "ko", "kf", "fault_step", "pad_args1", "gather_pause", "spec_rem", "argmax_slots", "pad_args2")
 
 
 class DfArgs(ctypes.Structure):
@@ -245,7 +245,8 @@ class DataflowDecoder:
         return (eng.tp_size == 1 and not eng.w.fp8 and cfg.n_embd in SUPPORTED_D and cfg.n_embd == 64 * cfg.n_head
                 and eng.w.ffn_local == 4 * cfg.n_embd)
 
-    def __init__(self, eng, grid: int | None = None, gs: int | None = None, j: int | None = None):
+    def __init__(self, eng, grid: int | None = None, gs: int | None = None, j: int | None = None,
+                 attn_split: str = "outputs"):
         if not self.supported(eng):
             raise ValueError("dataflow decode: TP=1 bf16 GPT-2 with d in %s only" % (SUPPORTED_D,))
         self.L = _bind_once()
@@ -262,8 +263,8 @@ class DataflowDecoder:
         gs = gs or int(os.environ.get("DLMS_DF_GS", "2"))
         # each head's 2 attention CUs split W_o by OUTPUT columns (d / 2 residual words each): 29.3
         # vs 30.5 ms at batch 1, 40.1 vs 41.4 at batch 2 against the head-dims split on one box
-        # (profiles/r4_df_sweep_v4.jsonl); DLMS_DF_ATTN_SPLIT=dims for the round-3 split
-        split = os.environ.get("DLMS_DF_ATTN_SPLIT", "outputs")
+        # (profiles/r4_df_sweep_v4.jsonl); assign(attn_split="dims") keeps the round-3 split for tests
+        split = attn_split
         while (cfg.n_head * gs > G or 64 % gs or (split == "outputs" and cfg.n_embd % (16 * gs))) and gs > 1:
             gs //= 2
         # MLP output groups J (see assign; each CU publishes d / J residual words of c_proj): 2 at
@@ -309,10 +310,45 @@ class DataflowDecoder:
         self._ring_bytes = {R: self._ring_bytes_for(R) for R in range(1, MAX_ROWS + 1)}
         self._window = ring_window(self.cus, cfg.n_embd, self.ko, self.kf, self.NC)
         self._exp_att, self._exp_mlp = expected_contributions(self.cus, self.COPIES)
-        # cooperative launch (the runtime guarantees the grid is co-resident); DLMS_DF_COOP=0: plain
-        self.coop = os.environ.get("DLMS_DF_COOP", "1") != "0"
         self._fault_step = -1
         self.launches = 0
+        self._args = {R: self._args_template(R) for R in range(1, MAX_ROWS + 1)}
+
+    def _args_template(self, R: int) -> DfArgs:
+        """The launch arguments that do not change between launches at R rows (the continuous
+        batcher launches once per decode chunk: per launch only the step count, penalty, scratch,
+        outputs and the test hook are set).  Fixed choices, each measured against its alternative:
+          * weight stream non-temporal: batch 1 28.1 -> 27.6-27.7 ms per query, GPT-2-medium 66.5 ->
+            65.7-66.0 (profiles/r4_df_nt_ab.jsonl);
+          * loaders pause while the comm wave polls a hand-off (MI355X_MICROARCH.md "gather-pass");
+          * residual poll: whole-row reads start 4 adds before the watched word completes: batch 1
+            28.8 -> 28.2 ms (1 / 2 / 8: 28.6 / 28.4 / 29.0), medium 66.7 -> 65.6
+            (profiles/r4_df_spec_poll_sweep.jsonl);
+          * per-step argmax through one key slot per CU instead of an atomic max + arrival counter:
+            28.2 -> 27.9 ms per query (profiles/r4_df_xf_slots_ab.jsonl)."""
+        eng, cfg, w = self.eng, self.eng.cfg, self.eng.w
+        a = DfArgs()
+        for name, t in (("packed", self.packed), ("cus", self.cu_tab), ("layers", self.layer_tab), ("wte", w.wte),
+                        ("wpe", w.wpe), ("lnf_g", w.lnf_g), ("lnf_b", w.lnf_b), ("lens", eng.lens),
+                        ("finished", eng.finished), ("out_tokens", eng.out_tokens), ("seen", eng.seen),
+                        ("cur_tok", eng.cur_tok), ("cur_pos", eng.cur_pos), ("cur_kvlen", eng.cur_kvlen),
+                        ("slots", self.slots), ("err", self.err)):
+            setattr(a, name, t.data_ptr())
+        a.step_words = self.step_words(R)
+        a.R, a.D, a.H, a.L = R, cfg.n_embd, cfg.n_head, cfg.n_layer
+        a.V, a.T, a.seen_words, a.eos = cfg.vocab_size, eng.max_length, eng.seen_words, cfg.eos_token_id
+        a.A, a.C, a.max_nq, a.swl = self.A, self.COPIES, self.max_nq, self.swl
+        a.ring_bytes, a.ldx, a.n_slots, a.P = self.ring_bytes(R), eng.x.stride(0), eng.max_batch, cfg.n_positions
+        a.eps = cfg.layer_norm_epsilon
+        a.nt_weights = 1
+        a.ko, a.kf = self.ko, self.kf
+        a.gather_pause = 1
+        a.spec_rem = 4
+        a.argmax_slots = int(cfg.vocab_size <= 65535 and self.G <= 256)
+        for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
+            a.exp_mlp[c] = self._exp_mlp[c]
+            a.exp_att[c] = self._exp_att[c]
+        return a
 
     def _ring_bytes_for(self, R: int) -> int:
         fixed = self.L.dlms_df_lds_fixed(self.eng.cfg.n_embd, R, self.max_nq, self.swl)
@@ -364,7 +400,7 @@ class DataflowDecoder:
         """``nsteps`` greedy decode steps (at most) of rows [0, B), B <= 2, on the current stream:
         exactly the state transitions of ``nsteps`` launch-per-op steps (decode_update semantics),
         stopping early once every row has finished."""
-        eng, cfg = self.eng, self.eng.cfg
+        eng = self.eng
         if not 1 <= B <= MAX_ROWS or nsteps <= 0:
             raise ValueError(f"dataflow run: B in [1, {MAX_ROWS}], nsteps > 0")
         if not self.fits(B):
@@ -373,46 +409,14 @@ class DataflowDecoder:
         if nsteps * self.max_step_bytes >= 2 ** 32 - 2 ** 24:
             raise ValueError("dataflow run: too many steps for one launch (32-bit stream offsets)")
         scratch = self._scratch_for(B, nsteps)
-        sw = self.step_words(B)
-        scratch[: sw * nsteps].zero_()
+        scratch[: self._args[B].step_words * nsteps].zero_()
         self.err.zero_()
-        a = DfArgs()
-        w = eng.w
-        for name, t in (("packed", self.packed), ("cus", self.cu_tab), ("layers", self.layer_tab), ("wte", w.wte),
-                        ("wpe", w.wpe), ("lnf_g", w.lnf_g), ("lnf_b", w.lnf_b), ("lens", eng.lens),
-                        ("finished", eng.finished), ("out_tokens", eng.out_tokens), ("seen", eng.seen),
-                        ("cur_tok", eng.cur_tok), ("cur_pos", eng.cur_pos), ("cur_kvlen", eng.cur_kvlen),
-                        ("slots", self.slots), ("scratch", scratch), ("err", self.err)):
-            setattr(a, name, t.data_ptr())
+        a = DfArgs.from_buffer_copy(self._args[B])
+        a.scratch = scratch.data_ptr()
         a.x_out = eng.x.data_ptr() if x_out else None
         a.trace = trace.data_ptr() if trace is not None else None
-        a.step_words = sw
-        a.R, a.D, a.H, a.L = B, cfg.n_embd, cfg.n_head, cfg.n_layer
-        a.V, a.T, a.seen_words, a.eos = cfg.vocab_size, eng.max_length, eng.seen_words, cfg.eos_token_id
-        a.nsteps, a.A, a.C, a.max_nq, a.swl = nsteps, self.A, self.COPIES, self.max_nq, self.swl
-        a.ring_bytes, a.ldx, a.n_slots, a.P = self.ring_bytes(B), eng.x.stride(0), eng.max_batch, cfg.n_positions
-        a.eps, a.penalty = cfg.layer_norm_epsilon, float(penalty)
-        # weight-stream cache policy: 0 default, 1 non-temporal, 2 non-temporal for the layers only.
-        # Non-temporal: batch 1 28.1 -> 27.6-27.7 ms per query (1 and 2 alike), GPT-2-medium 66.5 ->
-        # 65.7-66.0 with 1 (66.8 with 2) (profiles/r4_df_nt_ab.jsonl)
-        nt = os.environ.get("DLMS_DF_NT", "1")
-        a.nt_weights = int(nt) if nt in ("0", "1", "2") else 0
-        a.ko, a.kf = self.ko, self.kf
+        a.nsteps, a.penalty = nsteps, float(penalty)
         a.fault_step, self._fault_step = self._fault_step, -1
-        a.coop = int(self.coop)
-        a.gather_pause = int(os.environ.get("DLMS_DF_GATHER_PAUSE", "1") != "0")
-        # residual poll: whole-row reads start this many adds before the watched word completes
-        # (0: only once it has): batch 1 28.8 -> 28.2 ms at 4 (1 / 2 / 8: 28.6 / 28.4 / 29.0),
-        # GPT-2-medium 66.7 -> 65.6 (profiles/r4_df_spec_poll_sweep.jsonl); A/B knob DLMS_DF_SPEC
-        a.spec_rem = int(os.environ.get("DLMS_DF_SPEC", "4"))
-        # per-step argmax hand-off through one slot per CU instead of an atomic max + arrival counter
-        # (two round trips fewer per token): 28.2 -> 27.9 ms per query, GPT-2-medium -0.25 ms
-        # (profiles/r4_df_xf_slots_ab.jsonl); DLMS_DF_ARGMAX_SLOTS=0 for the counter (A/B)
-        a.argmax_slots = int(os.environ.get("DLMS_DF_ARGMAX_SLOTS", "1") != "0" and self.eng.cfg.vocab_size <= 65535
-                             and self.G <= 256)
-        for c in range(self.COPIES):  # contributions each fixed-point residual copy receives
-            a.exp_mlp[c] = self._exp_mlp[c]
-            a.exp_att[c] = self._exp_att[c]
         rc = self.L.dlms_dataflow_decode(ctypes.byref(a), self.G, _stream())
         if rc == NOT_RESIDENT:
             raise DataflowUnavailable(f"dataflow decode: a grid of {self.G} workgroups cannot be co-resident")

@@ -1,5 +1,7 @@
 """BERT gate: the torch reference encoder matches HF ``BertModel`` on the same weights (CPU,
 fp32, parity pinned against transformers), and the HIP encoder matches the reference (GPU)."""
+import time
+
 import pytest
 import torch
 
@@ -92,6 +94,33 @@ def test_gate_batches_concurrent_queries_cpu():
         assert abs(g_ - r_) < 1e-5
     assert gate.batched_queries == len(queries)
     assert gate.passes < len(queries)  # at least some queries shared a pass
+
+
+def test_check_async_cache_read_never_waits_on_an_encoder_pass():
+    """the aio front end reads the assignment-embedding cache on its event
+    loop; an encoder pass in progress (the gate's ``_lock`` held) must not stall that read."""
+    import asyncio
+
+    from distributed_lms_raft_llm_amd.gate.relevance import RelevanceGate
+
+    gate = RelevanceGate.create("bert-tiny", device="cpu", threshold=0.6)
+    text = "raft replicates a log"
+    gate.warm(text)
+    gate._lock.acquire()  # an encoder pass that takes a long time
+    try:
+        t0 = time.monotonic()
+        a = asyncio.run(asyncio.wait_for(asyncio.to_thread(lambda: gate._cache_get(gate._key(text))), 2.0))
+        assert a is not None and time.monotonic() - t0 < 1.0
+        # the full check_async: its cache read returns at once; the query itself waits for the pass
+        loop = asyncio.new_event_loop()
+        task = loop.create_task(gate.check_async("raft", text))
+        loop.run_until_complete(asyncio.sleep(0.05))
+        assert not task.done()  # parked on its batch, the loop kept running (this sleep returned)
+    finally:
+        gate._lock.release()
+    ok, s = loop.run_until_complete(asyncio.wait_for(task, 10.0))
+    loop.close()
+    assert ok == (s >= 0.6)
 
 
 @pytest.mark.gpu

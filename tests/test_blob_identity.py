@@ -132,8 +132,25 @@ def test_gc_spares_reuploaded_and_newly_referenced_objects(tmp_path):
     assert store.gc(set(), grace_s=3600.0) == 0 and store.has(old)
     # snapshot-time set says unreferenced, the live state now references it: kept
     os.utime(path, (time.time() - 7200, time.time() - 7200))
-    assert store.gc(set(), grace_s=3600.0, still_referenced=lambda sha: sha == old) == 0 and store.has(old)
-    assert store.gc(set(), grace_s=3600.0, still_referenced=lambda sha: False) == 1 and not store.has(old)
+    calls = []
+    assert store.gc(set(), grace_s=3600.0, live_refs=lambda: calls.append(1) or {old}) == 0 and store.has(old)
+    assert store.gc(set(), grace_s=3600.0, live_refs=lambda: calls.append(1) or set()) == 1 and not store.has(old)
+    assert len(calls) == 2  # the live set is built once per pass, not once per candidate
+    # a re-upload racing the unlink: _touch waits for the GC's re-check + unlink, then sees the
+    # object absent and the upload writes it again
+    old = store.put_bytes(b"racing content")
+    os.utime(store.cas_path(old), (time.time() - 7200, time.time() - 7200))
+    import threading
+
+    store._gc_lock.acquire()
+    t = threading.Thread(target=lambda: store.put_bytes(b"racing content"))
+    t.start()
+    time.sleep(0.05)
+    assert t.is_alive()  # the touch is parked behind the GC's lock
+    os.unlink(store.cas_path(old))  # what the GC does while holding it
+    store._gc_lock.release()
+    t.join(5)
+    assert store.has(old) and store.get_sha(old) == b"racing content"
 
 
 def test_login_and_logout_retries_are_idempotent(tmp_path):
