@@ -102,8 +102,9 @@ class _Rows:
     split_cap: int = 8  # split-K cap of the row-parallel projections (lower for concurrent row parts)
     split_fixed: int | None = None  # pinned split-K (M-independent arithmetic: prefill_split)
     persist_attn: bool = False  # decode attention as the low-occupancy persistent kernel
-    part: bool = False  # one of several concurrent row parts (no shared-workspace kernels)
     pidx: int = 0  # index of the row part (timing-only experiments address parts by it)
+    stats: torch.Tensor | None = None  # LN-folded step: row statistics [M, d/32, 2] of the residual
+    cnt: torch.Tensor | None = None  # ... and this part's split-K tile tickets
 
 
 class HostResult:
@@ -244,26 +245,24 @@ class HipGPT2Engine:
         # wave slots: 682.7 / 684.5 -> 691.5 / 691.1 k tok/s on one box; decode ms per generation over
         # three boxes: 256 blocks 169.2, 512 158.8, 768 157.9, 1024 160.1 (r2_sweep_persist_multistep.jsonl)
         self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "768"))
-        self.lm_skinny = os.environ.get("DLMS_LM_SKINNY", "0") == "1"  # measured neutral at B=1 (profiles/r2_lm_head_b1.txt)
-        # latency path, TP=1: ln_f fused into a skinny LM head (one kernel fewer per token) -- opt-in:
-        # the skinny LM head is slower than the tiled one by more than the launch it saves
-        # (batch 1: 37.3 vs 35.9 ms per query, profiles/r2_lm_head_b1.txt)
-        self.lm_ln_fused = os.environ.get("DLMS_LM_LN_FUSED", "0") == "1"
-        self.alt_attn = os.environ.get("DLMS_OVERLAP_ALT_ATTN", "0") == "1"
-        # overlapped step, TP=1 bf16: LN2 folded into c_fc (ops.fold_ln_weights / EPI_GELU_LN) -- the
-        # out-projection updates the residual in place and leaves a bf16 copy, c_fc normalises
-        # algebraically from its own A fragments: one launch fewer per layer and row part.  OPT-IN:
-        # measured 5 % slower at 1024 queries (688-690 vs 724 k tok/s, profiles/r3_fold_ln2_and_interference.jsonl):
-        # the out-projection loses its split-K (32x64 full-K tiles, 147 KB per workgroup) and c_fc's
-        # K loop carries the statistics, which together cost more than the LayerNorm launch saved
-        self.fold_ln2 = (os.environ.get("DLMS_FOLD_LN2", "0") == "1" and self.tp_size == 1 and not self.w.fp8
-                         and self.overlap)
-        self._ln2_fold = None
-        if self.fold_ln2:
-            self._ln2_fold = [ops.fold_ln_weights(lw.ln2_g, lw.ln2_b, lw.w_fc, lw.b_fc) for lw in self.w.layers]
-        # 16-32 rows: this many latency-path parts on as many HIP streams (0/1 = off)
-        self.small_overlap_parts = int(os.environ.get("DLMS_SMALL_OVERLAP_PARTS", "0"))  # measured slower (docs/PERFORMANCE.md)
-        self._in_small_overlap = False
+        # (measured and removed: a skinny MFMA LM head at B <= 8, neutral at batch 1, and ln_f fused
+        # into it, 37.3 vs 35.9 ms per query -- profiles/r2_lm_head_b1.txt)
+        # overlapped step (the 1024-query headline), TP=1 bf16: LayerNorms folded into the GEMMs.  The
+        # out-projection and c_proj update the residual in place (EPI_RESID_LN: split-K slices reduced
+        # in the kernel by the last arriving slice), leave a bf16 copy and per-row statistics; c_fc and
+        # the next layer's QKV apply LN2 / LN1 algebraically in their epilogues (ops.fold_ln_weights):
+        # 23 of the 25 add+LayerNorm launches per row half and step are gone.  DLMS_LN_FOLD=0: off.
+        fold_env = os.environ.get("DLMS_LN_FOLD", "0")
+        self.ln_fold = (self.tp_size == 1 and not self.w.fp8 and self.overlap and cfg.n_embd % ops.LN_SLICE == 0
+                        and cfg.n_embd // ops.LN_SLICE <= ops.LNF_MAX_SLOTS and fold_env != "0")
+        self.ln_fold_mode = fold_env  # EXPERIMENT: "1" both LNs, "2" LN2 only (out-proj unsplit), "3" LN2 only split 2
+        self._fold_qkv = self._fold_fc = None
+        if self.ln_fold:
+            L = self.w.layers
+            self._fold_qkv = [None] + [ops.fold_ln_weights(lw.ln1_g, lw.ln1_b, lw.w_qkv, lw.b_qkv) for lw in L[1:]]
+            self._fold_fc = [ops.fold_ln_weights(lw.ln2_g, lw.ln2_b, lw.w_fc, lw.b_fc) for lw in L]
+        # (measured and removed: 16-32 rows as latency-path parts on several HIP streams, slower than
+        # the tiled step -- profiles/r2_sweep_small_overlap.jsonl)
         self.prefill_graphs = os.environ.get("DLMS_PREFILL_GRAPH", "1") != "0"
         self._pgraphs: dict[tuple[int, int], dict] = {}
         self._pseen: dict[tuple[int, int], int] = {}
@@ -310,13 +309,11 @@ class HipGPT2Engine:
                 if lw.w_o_sh is None:
                     lw.w_o_sh = ops.shuffle_weight(lw.w_o)
             self.ao_parts = torch.zeros(self.w.n_heads_local, 4, cfg.n_embd, dtype=torch.float32, device=self.device)
-        # batch 1: head groups of H/4 (3 or 4 heads) -> 4 slabs (DLMS_AO_GROUPS=0: one slab per head)
+        # batch 1: head groups of H/4 (3 or 4 heads) -> 4 slabs, 3 W_o tiles per workgroup
+        # (profiles/r2_attn_oproj_ab.txt: 36.6 vs 37.1 ms per query with one slab per head)
         Hl = self.w.n_heads_local
-        self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4) and
-                                      os.environ.get("DLMS_AO_GROUPS", "1") != "0") else 0
-        self.ao_group_tiles = int(os.environ.get("DLMS_AO_GROUP_TILES", "3"))
-        if self.ao_groups and (cfg.n_embd // 16) % self.ao_group_tiles:
-            self.ao_group_tiles = 1
+        self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4)) else 0
+        self.ao_group_tiles = 3 if (cfg.n_embd // 16) % 3 == 0 else 1
         # batch 1 (TP=1, head-grouped attention): LN2 -> c_fc -> GELU -> c_proj as ONE kernel whose
         # workgroups add their 16-column slices into an int64 fixed-point residual (order-independent
         # integer atomics; ops.skinny_mlp) -- one launch and one dependent round trip fewer per layer
@@ -359,8 +356,7 @@ class HipGPT2Engine:
                  64 * (2 * cfg.n_embd + 32) + 8 * 4096 <= ops.PS_LDS_BYTES and
                  os.environ.get("DLMS_PS_LMHEAD", "1") != "0")
         self.ps_lm = ps_lm and not self.w.fp8
-        if not self.w.fp8 and (ps_lm or (self.small_max > 0 and (self.lm_skinny or self.lm_ln_fused))):
-            # (the latency path's skinny LM head reads the same pre-shuffled copy)
+        if self.ps_lm:
             self.lm_head_sh = ops.shuffle_weight(self.w.lm_head)
         # batch 1 (TP=1, bf16): the persistent dataflow decode -- one launch per chunk of decode steps
         # (ops/dataflow.py); built on first use (it packs a per-CU copy of the weights).  Default ON
@@ -411,6 +407,9 @@ class HipGPT2Engine:
         # cross-workgroup split attention (few rows, long caches): partials + arrival counters
         self.attn_ws = ops.AttnSplitWorkspace(self.SPLIT_ATTN_MAX_PAIRS, 2, dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
+        if self.ln_fold:  # LN-folded overlapped step: row statistics and per-part split-K tile tickets
+            self.ln_stats = torch.zeros(B, D // ops.LN_SLICE, 2, dtype=f32, device=dev)
+            self.tile_cnt = torch.zeros(self.overlap_parts, -(-B // 64) * (D // 64), dtype=torch.int32, device=dev)
         self.h = torch.zeros(B, D, dtype=bf, device=dev)
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.att = torch.zeros(B, Dl, dtype=bf, device=dev)
@@ -565,10 +564,6 @@ class HipGPT2Engine:
         elif r.M * self.w.n_heads_local <= self.SPLIT_ATTN_MAX_PAIRS:
             # decode with few (row, head) pairs: split-K flash-decode puts NW waves on each pair's keys
             nw, ns = ops.attention_split_geometry(r.M * self.w.n_heads_local, self.max_length)
-            if r.part:
-                # concurrent row parts (multi-stream small step) would share the one workspace's
-                # partials and arrival counters: keep each (row, head) pair in one workgroup
-                ns = 1
             ops.attention_split(r.q, self.kv[li, 0], self.kv[li, 1], r.row_slot, r.row_kvlen, out=r.att,
                                 waves=nw, splits=ns, workspace=self.attn_ws if ns > 1 else None)
         elif r.persist_attn:
@@ -580,15 +575,6 @@ class HipGPT2Engine:
 
     def _attn_out_mlp(self, r: "_Rows", li: int):
         """out-proj -> LN2 -> c_fc + GELU -> c_proj; leaves c_proj's residual update pending."""
-        if r.persist_attn and self._ln2_fold is not None and not self._skip(r):
-            # LN2 folded into c_fc: x += att W_o^T + b_o in place (+ bf16 copy into h, which the QKV
-            # GEMM has consumed), then c_fc normalises its raw A rows algebraically
-            lw = self.w.layers[li]
-            wp, c1, c2 = self._ln2_fold[li]
-            ops.gemm(r.att, lw.w_o, ops.EPI_F32X2, bias=lw.b_o, resid=r.x, out=r.x, out2=r.h)
-            ops.gemm(r.h, wp, ops.EPI_GELU_LN, bias=c2, ln_c1=c1, ln_eps=self.cfg.layer_norm_epsilon, out=r.ff)
-            r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap, r.split_fixed)
-            return
         if self._skip(r) in ("gemm", "ln", "all"):  # timing-only experiment: see __init__
             if self._skip(r) == "ln":
                 lw = self.w.layers[li]
@@ -631,24 +617,17 @@ class HipGPT2Engine:
         self._final_ln(r, final_h)
 
     def _lm_head_and_update(self, hidden: torch.Tensor | None, B: int, penalty: float, seen: torch.Tensor | None = None,
-                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0,
-                            keys_ready: bool = False):
+                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0):
         """LM head with the fused penalty + argmax on ``hidden`` (bf16, or e4m3 with ``hscale``),
         then the greedy bookkeeping.  Rows map to slots [lo, lo + B) or through ``slot_map``."""
         cfg = self.cfg
         hi = lo + B
         seen_rows = self.seen[lo:hi] if seen is None else seen
         P = self.key_parts.shape[1]  # partial keys per row the LM head writes (and the consumer reads)
-        if keys_ready:  # the caller ran the LM head (skinny, ln_f fused): one key per 64 columns
-            P = self.lm_head_sh.shape[0] * 16 // 64
-        elif hidden.dtype != ops.FP8 and self.ps_lm and B >= self.PS_LM_MIN_ROWS:
+        if hidden.dtype != ops.FP8 and self.ps_lm and B >= self.PS_LM_MIN_ROWS:
             P = ops.gemm_ps_key_slots(B, self.lm_head_sh.shape[0] * 16, self.lm_head_sh.shape[1] * 32)
             ops.gemm_ps(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                         vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
-        elif hidden.dtype != ops.FP8 and self.lm_head_sh is not None and B <= self.small_max and self.lm_skinny:
-            # latency path: pre-shuffled skinny MFMA LM head (non-temporal weight stream)
-            ops.skinny_gemm(hidden, self.lm_head_sh, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi],
-                            seen=seen_rows, vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty)
         elif hidden.dtype == ops.FP8:
             ops.gemm(hidden, self.w.lm_head8, ops.EPI_ARGMAX, argmax_out=self.key_parts[lo:hi], seen=seen_rows,
                      vocab=cfg.vocab_size, col_offset=self.w.vocab_range[0], penalty=penalty, a_scale=hscale,
@@ -683,10 +662,14 @@ class HipGPT2Engine:
         r.split_cap = self.overlap_split_cap
         r.persist_attn = self.persist_attn_blocks > 0
         r.pidx = lo // max(1, hi - lo)
+        if self.ln_fold:
+            r.stats, r.cnt = self.ln_stats[lo:hi], self.tile_cnt[r.pidx]
         return r
 
     def _part_step(self, r: "_Rows", lo: int, penalty: float):
         """The whole decode step for one row range (rows are independent sequences)."""
+        if self.ln_fold and r.stats is not None and not self._skip(r):
+            return self._part_step_folded(r, lo, penalty)
         for li in range(len(self.w.layers)):
             self._attn_in(r, li)
             self._attn(r, li)
@@ -697,17 +680,61 @@ class HipGPT2Engine:
         else:
             self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
 
+    def _fold_split(self, K: int, want: int) -> int:
+        return max(d for d in range(1, want + 1) if (K // 64) % d == 0)
+
+    def _part_step_folded(self, r: "_Rows", lo: int, penalty: float):
+        """One row range's decode step with the LayerNorms folded into the GEMMs: per layer
+        QKV (LN1 in its epilogue; layer 0: a standalone LN1 of the embedding rows) -> attention ->
+        out-projection updating x in place (+ bf16 copy + row statistics) -> c_fc + GELU (LN2 in
+        its epilogue) -> c_proj updating x in place; then ln_f and the LM head.  Five launches per
+        layer instead of seven; the split-K slices of the two residual projections are reduced by
+        their last arriving slice (gemm.hip EPI_RESID_LN)."""
+        eps, D = self.cfg.layer_norm_epsilon, self.cfg.n_embd
+        so, sp = self._fold_split(self.w.d_local, 2), self._fold_split(self.w.ffn_local, 4)
+        mode = self.ln_fold_mode
+        if mode == "2":
+            so = 1
+        for li, lw in enumerate(self.w.layers):
+            kc, vc = self.kv[li, 0], self.kv[li, 1]
+            if mode in ("2", "3"):
+                ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, parts=r.pend[0], nsplit=r.pend[1], bias=r.pend[2],
+                                  out_bf16=r.h)
+                ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
+                         row_slot=r.row_slot, row_pos=r.row_pos)
+            elif li == 0:
+                ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, out_bf16=r.h)
+                ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
+                         row_slot=r.row_slot, row_pos=r.row_pos)
+            else:
+                wq, c1, c2 = self._fold_qkv[li]
+                ops.gemm(r.h, wq, ops.EPI_QKV, bias=c2, ln_c1=c1, ln_eps=eps, ln_stats=r.stats, q_out=r.q,
+                         k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
+            self._attn(r, li)
+            ops.gemm(r.att, lw.w_o, ops.EPI_RESID_LN, bias=lw.b_o, resid=r.x, out=r.x, out2=r.h, ln_stats=r.stats,
+                     split_k=so, ws=r.parts, tile_cnt=r.cnt)
+            wf, c1, c2 = self._fold_fc[li]
+            ops.gemm(r.h, wf, ops.EPI_GELU_TANH, bias=c2, ln_c1=c1, ln_eps=eps, ln_stats=r.stats, out=r.ff)
+            if mode in ("2", "3"):
+                r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap, r.split_fixed)
+            else:
+                ops.gemm(r.ff, lw.w_p, ops.EPI_RESID_LN, bias=lw.b_p, resid=r.x, out=r.x, out2=r.h, ln_stats=r.stats,
+                         split_k=sp, ws=r.parts, tile_cnt=r.cnt)
+        if mode in ("2", "3"):
+            self._final_ln(r, r.h)
+        else:
+            ops.add_layernorm(r.x, self.w.lnf_g, self.w.lnf_b, eps, out_bf16=r.h)
+        self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
+
     def _decode_step_overlap(self, B: int, penalty: float, nsteps: int = 1):
         """Decode step as ``overlap_parts`` row ranges on as many HIP streams (one hardware queue
         each), free-running: the decode GEMMs are latency-bound (a near-constant ~12 us per launch
         whatever M, profiles/r1_gemm_lab) and attention is HBM-bound, so independent row ranges
         fill each other's bubbles -- the GEMMs of one part run beside the KV stream and the GEMMs
         of the others.  Captured as one hipGraph with ``overlap_parts`` independent branches (fork
-        at the start, join at the end).
-
-        ``DLMS_OVERLAP_SERIAL=1`` (two parts only): GEMM phases of the halves serialised by
-        cross-stream events so attention of one half always pairs with the GEMMs of the other
-        (measured slower: the halves' GEMMs then cannot overlap each other)."""
+        at the start, join at the end).  (Measured and removed: the halves' GEMM phases serialised
+        so attention of one always pairs with the GEMMs of the other, and the attentions forced to
+        alternate on HBM -- both slower, profiles/r2_sweep_alt_attn.jsonl.)"""
         k = self.overlap_parts
         cur = torch.cuda.current_stream(self.device)
         while len(self._side_streams) < k - 1:
@@ -717,74 +744,14 @@ class HipGPT2Engine:
             s.wait_stream(cur)
         step = B // k
         parts = [(i * step, self._part_rows(i * step, (i + 1) * step)) for i in range(k)]
-        def fresh(i):  # per-step row state (the pending residual update must not carry across steps)
-            return parts if i == 0 else [(lo, self._part_rows(lo, lo + step)) for lo, _ in parts]
-
-        if k == 2 and os.environ.get("DLMS_OVERLAP_SERIAL", "0") == "1":
-            for i in range(nsteps):
-                self._two_halves_serialised(fresh(i), streams, penalty)
-        elif self.alt_attn:
-            for i in range(nsteps):
-                self._alternating_attention(fresh(i), streams, penalty)
-        else:
-            for (lo, r), s in zip(parts, streams):
-                with torch.cuda.stream(s):
-                    for i in range(nsteps):
-                        # (fresh row state per step: _Rows carries the residual update pending
-                        # between layers, which the last layer of a step leaves set)
-                        self._part_step(r if i == 0 else self._part_rows(lo, lo + step), lo, penalty)
-        for s in streams[1:]:
-            cur.wait_stream(s)
-
-    def _alternating_attention(self, parts, streams, penalty: float):
-        """Attention kernels of the row ranges take turns on HBM (part 0 layer l, part 1 layer l, ...,
-        part 0 layer l + 1): each waits for the previous one to finish, so the KV stream of one part
-        always runs beside the GEMM-side chain of the others instead of all parts' attentions
-        colliding at the same time (free-running identical chains fall into phase)."""
-        last = None
-        for li in range(len(self.w.layers)):
-            for (lo, r), s in zip(parts, streams):
-                with torch.cuda.stream(s):
-                    self._attn_in(r, li)
-                    if last is not None:
-                        s.wait_event(last)
-                    self._attn(r, li)
-                    last = torch.cuda.Event()
-                    last.record(s)
-                    self._attn_out_mlp(r, li)
         for (lo, r), s in zip(parts, streams):
             with torch.cuda.stream(s):
-                self._final_ln(r, r.h)
-                if self.w.fp8:
-                    self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
-                else:
-                    self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
-
-    def _two_halves_serialised(self, halves, streams, penalty: float):
-        """Phases G(0) A(0) G(1) ... A(L-1) G(L) per half (G(l) = out-proj/LN2/c_fc/c_proj of
-        layer l-1 + LN1/QKV of layer l; G(L) ends in ln_f + LM head + update; A(l) = attention),
-        GEMM phases alternating between the halves (G_a(l) -> G_b(l) -> G_a(l+1) ...)."""
-        L = len(self.w.layers)
-        last_gemm = None
-        for p in range(L + 1):
-            for (lo, r), s in zip(halves, streams):
-                with torch.cuda.stream(s):
-                    if last_gemm is not None:
-                        s.wait_event(last_gemm)
-                    if p > 0:
-                        self._attn_out_mlp(r, p - 1)
-                    if p < L:
-                        self._attn_in(r, p)
-                    else:
-                        self._final_ln(r, r.h)
-                        if self.w.fp8:
-                            self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
-                        else:
-                            self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
-                    last_gemm = torch.cuda.Event()
-                    last_gemm.record(s)
-                    if p < L:
-                        self._attn(r, p)
+                for i in range(nsteps):
+                    # (fresh row state per step: _Rows carries the residual update pending
+                    # between layers, which the last layer of a step leaves set)
+                    self._part_step(r if i == 0 else self._part_rows(lo, lo + step), lo, penalty)
+        for s in streams[1:]:
+            cur.wait_stream(s)
 
     def _df_supported(self) -> bool:
         from ..ops.dataflow import DataflowDecoder
@@ -859,7 +826,6 @@ class HipGPT2Engine:
         hi = lo + B
         r = self._rows(self.x[lo:hi], self.parts[:, lo:hi], self.h[lo:hi], self.q[lo:hi], self.att[lo:hi],
                        self.ff[lo:hi], self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], B)
-        r.part = self._in_small_overlap
         bufs = (self.x[lo:hi], self.x2[lo:hi])
         cur = 0
         pend = None  # (nsplit, residual bias) still to be added into x
@@ -878,7 +844,7 @@ class HipGPT2Engine:
                 self._all_reduce(self.parts[0, :B])
             return split
 
-        if inplace and self.fused_mlp and B <= max(1, self.fused_mlp_rows) and not r.part and not lo:
+        if inplace and self.fused_mlp and B <= max(1, self.fused_mlp_rows):
             self._decode_layers_fused_mlp(r, B)
             ops.ln_fix(self.xr[(len(self.w.layers) - 1) % 2, :, :B], self.w.lnf_g, self.w.lnf_b, eps, self.h[:B])
             self._lm_head_and_update(self.h[:B], B, penalty)
@@ -898,12 +864,12 @@ class HipGPT2Engine:
                                       parts=parts, nsplit=pend[0], res_bias=pend[1], bias=lw.b_qkv, q_out=r.q,
                                       k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
                 cur = 1 - cur
-            if self.fuse_ao and B == 1 and self.ao_groups and not r.part:
+            if self.fuse_ao and B == 1 and self.ao_groups:
                 # heads in groups of H/4: exactly the 4 slabs the fused add+LN sums cheaply
                 ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
                                             self.ao_groups, tiles=self.ao_group_tiles)
                 mlp_parts, ns, rb = self.ao_parts[:4, :1], 4, lw.b_o
-            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS and not r.part:
+            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
                 ops.attention_oproj(self.q[:B], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts)
                 mlp_parts, ns, rb = self.ao_parts[:, :B], self.w.n_heads_local, lw.b_o
             elif inplace:
@@ -926,13 +892,6 @@ class HipGPT2Engine:
                 pend = None
             else:
                 pend = (row_parallel(r.ff, lw.w_p), lw.b_p)
-        if pend is None and self.lm_ln_fused and not lo:
-            # ln_f in the LM head's prologue: every workgroup normalises the (few) rows itself
-            ops.skinny_gemm(bufs[cur], self.lm_head_sh, ops.EPI_ARGMAX, ln=(self.w.lnf_g, self.w.lnf_b, eps),
-                            argmax_out=self.key_parts[:B], seen=self.seen[:B], vocab=self.cfg.vocab_size,
-                            col_offset=self.w.vocab_range[0], penalty=penalty)
-            self._lm_head_and_update(None, B, penalty, keys_ready=True)
-            return
         if pend is None:
             ops.add_layernorm(bufs[cur], self.w.lnf_g, self.w.lnf_b, eps, out_bf16=self.h[lo:hi])
         else:
@@ -987,44 +946,15 @@ class HipGPT2Engine:
             self._all_reduce_i64(acc_all)
             xin = acc_all[:, :B]
 
-    def _small_overlap_ok(self, B: int) -> bool:
-        k = self.small_overlap_parts
-        return (k > 1 and self.small_inplace and B > self.small_max and B % k == 0 and
-                B // k <= self.small_max and B <= self.x2.shape[0])
-
-    def _decode_step_small_overlap(self, B: int, penalty: float):
-        """16-32 rows as ``small_overlap_parts`` latency-path parts of <= small_max rows on as many
-        HIP streams: every kernel of the small step fills only a fraction of the CUs (36-192
-        workgroups), so independent row ranges run side by side instead of one tiled chain."""
-        k = self.small_overlap_parts
-        cur = torch.cuda.current_stream(self.device)
-        while len(self._side_streams) < k - 1:
-            self._side_streams.append(torch.cuda.Stream(device=self.device))
-        streams = [cur] + self._side_streams[: k - 1]
-        for s in streams[1:]:
-            s.wait_stream(cur)
-        step = B // k
-        self._in_small_overlap = True
-        try:
-            for i, s in enumerate(streams):
-                with torch.cuda.stream(s):
-                    self._decode_step_small(step, penalty, lo=i * step)
-        finally:
-            self._in_small_overlap = False
-        for s in streams[1:]:
-            cur.wait_stream(s)
-
     def _decode_step(self, B: int, penalty: float, nsteps: int = 1):
         if nsteps > 1:
-            if self._overlap_ok(B) and not self._small_ok(B) and not self._small_overlap_ok(B):
+            if self._overlap_ok(B) and not self._small_ok(B):
                 return self._decode_step_overlap(B, penalty, nsteps)
             for _ in range(nsteps):
                 self._decode_step(B, penalty)
             return
         if self._small_ok(B):
             return self._decode_step_small(B, penalty)
-        if self._small_overlap_ok(B):
-            return self._decode_step_small_overlap(B, penalty)
         if self._overlap_ok(B):
             return self._decode_step_overlap(B, penalty)
         self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
@@ -1279,7 +1209,7 @@ class HipGPT2Engine:
 
     def _steps_per_graph_for(self, B: int) -> int:
         """Decode steps per graph replay for a batch bucket (DLMS_STEPS_PER_GRAPH[_SMALL])."""
-        overlapped = self._overlap_ok(B) and not self._small_ok(B) and not self._small_overlap_ok(B)
+        overlapped = self._overlap_ok(B) and not self._small_ok(B)
         return self.steps_per_graph if overlapped else self.steps_per_graph_small
 
     def health_async(self) -> "HostResult | None":

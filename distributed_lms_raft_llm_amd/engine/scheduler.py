@@ -218,12 +218,16 @@ class ContinuousBatcher:
             if steps > 0:
                 B = min(_bucket(max(self._active) + 1), eng.max_batch)
                 td = time.perf_counter()
+                # the budget each live request actually gives up to this chunk (a request near its
+                # max_length gives less than `steps`): an aborted chunk refunds exactly that
+                taken = {}
+                for s, r in self._active.items():
+                    taken[s] = min(steps, r.steps_left)
+                    r.steps_left -= taken[s]
                 with roctx_range("decode_chunk"):
                     eng.decode(B, steps, self.penalty)
                     cur = (flags_async(eng, B), dict(self._active), health_async(eng), dataflow_status_async(eng),
-                           steps)
-                for r in self._active.values():
-                    r.steps_left = max(0, r.steps_left - steps)
+                           taken)
                 self.steps += steps
                 TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
                                 steps=steps)
@@ -243,7 +247,7 @@ class ContinuousBatcher:
                     METRICS.inc(f"{self.name}_dataflow_aborts")
                     for s, r in prev[1].items():
                         if self._active.get(s) is r:
-                            r.steps_left += prev[4]
+                            r.steps_left += prev[4].get(s, 0)
                 # by identity: a slot retired one chunk earlier may already hold a new request
                 done = [s for s, r in prev[1].items() if s < len(flags) and flags[s] and self._active.get(s) is r]
                 if done:

@@ -35,7 +35,9 @@ SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "en
            "dataflow.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
-EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL, EPI_F32X2, EPI_GELU_LN = range(9)
+EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL, EPI_RESID_LN = range(8)
+LN_SLICE = 32        # columns per LayerNorm-statistics slot (gemm.hip EPI_RESID_LN -> MODE_LNF)
+LNF_MAX_SLOTS = 32   # a folded consumer reads at most this many slots per row (d <= 1024)
 
 _lock = threading.Lock()
 _lib = None
@@ -119,6 +121,8 @@ class GemmEpi(ctypes.Structure):
         ("a_scale", ctypes.c_void_p), ("w_scale", ctypes.c_void_p),
         ("n_slots", ctypes.c_int),
         ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int), ("ln_c1", ctypes.c_void_p), ("ln_eps", ctypes.c_float),
+        ("ln_stats", ctypes.c_void_p), ("ln_nst", ctypes.c_int), ("ln_k", ctypes.c_int), ("ln_fold", ctypes.c_int),
+        ("ws", ctypes.c_void_p), ("ldws", ctypes.c_int), ("tile_cnt", ctypes.c_void_p),
     ]
 
 
@@ -298,10 +302,20 @@ def _req(t: torch.Tensor, dtype, name: str, dim: int | None = None):
 def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, out=None, resid=None,
          q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
          argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0,
-         split_k: int = 1, a_scale=None, w_scale=None, out2=None, ln_c1=None, ln_eps: float = 1e-5):
+         split_k: int = 1, a_scale=None, w_scale=None, out2=None, ln_c1=None, ln_eps: float = 1e-5,
+         ln_stats=None, ws=None, tile_cnt=None):
     """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0).
     fp8 (W8A8): a and w ``torch.float8_e4m3fn`` with f32 ``a_scale`` [M] and ``w_scale`` [N]
-    (C = diag(a_scale) (a @ w.T) diag(w_scale)); K % 128 == 0."""
+    (C = diag(a_scale) (a @ w.T) diag(w_scale)); K % 128 == 0.
+
+    ``EPI_RESID_LN`` (residual projection of the LayerNorm-folded decode chain): ``out`` (f32
+    [M, N], normally the residual ``resid`` itself) = resid + a w^T + bias, ``out2`` = its bf16
+    copy, ``ln_stats`` (f32 [M, >= N/32, 2]) = each row's (sum, sum of squares) per 32 columns;
+    ``split_k`` > 1 needs ``ws`` (f32 [>= split_k, M, N] slice partials) and ``tile_cnt`` (int32,
+    zero, one per output tile: the kernel leaves it zero).
+    ``ln_stats`` with EPI_QKV / EPI_GELU_TANH / EPI_BF16 (and ``ln_c1``): LayerNorm folded in --
+    ``a`` is the raw bf16 residual, ``w``/``ln_c1``/``bias`` the ``fold_ln_weights`` triple, the
+    row statistics those of an EPI_RESID_LN producer over K columns."""
     fp8 = a.dtype == FP8
     _req(a, FP8 if fp8 else torch.bfloat16, "a", 2)
     _req(w, FP8 if fp8 else torch.bfloat16, "w", 2)
@@ -322,20 +336,53 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         if bias.numel() < N:
             raise ValueError("bias too short")
         ep.bias = bias.data_ptr()
-    if epi in (EPI_F32X2, EPI_GELU_LN) and fp8:
-        raise ValueError("EPI_F32X2 / EPI_GELU_LN: bf16 inputs only")
-    if epi == EPI_F32X2:
+    if epi == EPI_RESID_LN:
+        if fp8:
+            raise ValueError("EPI_RESID_LN: bf16 inputs only")
+        if N % LN_SLICE:
+            raise ValueError(f"EPI_RESID_LN: N % {LN_SLICE}")
+        _req(out, torch.float32, "out", 2)
+        _req(resid, torch.float32, "resid", 2)
         _req(out2, torch.bfloat16, "out2", 2)
-        if out2.shape[0] < M or out2.shape[1] < N or out2.stride(1) != 1:
-            raise ValueError("out2 too small")
+        _req(ln_stats, torch.float32, "ln_stats", 3)
+        if out.shape[0] < M or out.shape[1] < N or resid.shape[0] < M or resid.shape[1] < N or \
+                out2.shape[0] < M or out2.shape[1] < N or ln_stats.shape[0] < M or ln_stats.shape[1] * LN_SLICE < N \
+                or ln_stats.shape[2] != 2 or not ln_stats.is_contiguous():
+            raise ValueError("EPI_RESID_LN buffers too small")
+        for t in (out, resid, out2):
+            if t.data_ptr() % 16 or t.stride(0) % 8:
+                raise ValueError("EPI_RESID_LN: rows must be 16-byte aligned")
+        if split_k < 1 or K % (64 * split_k):
+            raise ValueError(f"split_k={split_k} must divide K/64 (K={K})")
+        ep.out, ep.ldo, ep.resid, ep.ldr = out.data_ptr(), out.stride(0), resid.data_ptr(), resid.stride(0)
         ep.out2, ep.ldo2 = out2.data_ptr(), out2.stride(0)
-    if epi == EPI_GELU_LN:
+        ep.ln_stats, ep.ln_nst = ln_stats.data_ptr(), ln_stats.shape[1]
+        ep.split_k = split_k
+        if split_k > 1:
+            _req(ws, torch.float32, "ws", 3)
+            _req(tile_cnt, torch.int32, "tile_cnt", 1)
+            tiles = -(-M // 64) * (N // 64)
+            if ws.shape[0] < split_k or ws.shape[1] < M or ws.shape[2] < N or ws.stride(1) % 4 or ws.data_ptr() % 16 \
+                    or tile_cnt.numel() < tiles or ws.stride(0) * split_k * 4 >= 2 ** 31:
+                raise ValueError("EPI_RESID_LN: split-K workspace / tile counters too small")
+            ep.ws, ep.ldws, ep.split_stride, ep.tile_cnt = ws.data_ptr(), ws.stride(1), ws.stride(0), tile_cnt.data_ptr()
+        _check(lib().dlms_gemm(epi, _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, ctypes.byref(ep), _stream()),
+               "dlms_gemm")
+        return out
+    if ln_stats is not None:
+        if fp8 or epi not in (EPI_QKV, EPI_GELU_TANH, EPI_BF16):
+            raise ValueError("folded LayerNorm: bf16 QKV / GELU / bf16 epilogues only")
+        _req(ln_stats, torch.float32, "ln_stats", 3)
         _req(ln_c1, torch.float32, "ln_c1", 1)
-        if ln_c1.numel() < N:
-            raise ValueError("ln_c1 too short")
+        nst = ln_stats.shape[1]
+        if ln_stats.shape[0] < M or nst * LN_SLICE != K or nst > LNF_MAX_SLOTS or ln_c1.numel() < N or \
+                not ln_stats.is_contiguous() or ln_stats.shape[2] != 2:
+            raise ValueError(f"folded LayerNorm: statistics [M, K/{LN_SLICE}, 2] (K <= {LN_SLICE * LNF_MAX_SLOTS}) "
+                             f"and c1 [N] needed")
+        ep.ln_stats, ep.ln_nst, ep.ln_k, ep.ln_fold = ln_stats.data_ptr(), nst, K, 1
         ep.ln_c1, ep.ln_eps = ln_c1.data_ptr(), float(ln_eps)
-    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_F32X2, EPI_GELU_LN):
-        want = torch.float32 if epi in (EPI_F32, EPI_F32X2) else torch.bfloat16
+    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32):
+        want = torch.float32 if epi == EPI_F32 else torch.bfloat16
         if out is None:
             out = torch.empty(M, N, dtype=want, device=a.device)
         _req(out, want, "out", 2)
@@ -728,7 +775,7 @@ SKINNY_MAX_M = 32
 
 
 def fold_ln_weights(gamma: torch.Tensor, beta: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None):
-    """LayerNorm folded into the following GEMM (``EPI_GELU_LN``): LN(x) W^T + b = rstd (x W'^T - mu c1)
+    """LayerNorm folded into the following GEMM (``gemm(..., ln_stats=...)``): LN(x) W^T + b = rstd (x W'^T - mu c1)
     + c2 with W' = bf16(gamma (.) W) (the operand the MFMAs see), c1 = row sums of that bf16 W' in
     fp32, c2 = beta W^T + b.  w: bf16 [N, K]; gamma, beta: f32 [K].  Returns (W', c1, c2)."""
     wf = w.float()
@@ -1096,7 +1143,9 @@ def attention_split_waves(kv_len_max: int) -> int:
 
 
 ATTN_WS_STRIDE = 68  # floats per cross-workgroup partial (skinny.hip)
-ATTN_SPLIT_SYNC = int(os.environ.get("DLMS_ATTN_SPLIT_SYNC", "2"))
+# publish mode of the cross-workgroup split attention: write-through partials + a vmcnt wait (0:
+# __threadfence, 2x slower; 1: write-through + agent fences) -- profiles/r2_attn_splitwg.jsonl
+ATTN_SPLIT_SYNC = 2
 
 
 def attention_split_geometry(pairs: int, kv_len_max: int, cus: int = 256) -> tuple[int, int]:
@@ -1256,13 +1305,8 @@ def gemm_ps_geometry(M: int, N: int, epi: int, split: int = 1, cus: int = 256, K
     kc = K // max(1, split)
     fits4 = 64 * (kc * 2 + 32) + 8 * 4096 <= PS_LDS_BYTES
     mt = 4 if ((epi == EPI_ARGMAX or M >= 512) and fits4) else 2
-    # LM head: 80-row panels (DLMS_PS_MT=5) where they take fewer row blocks (512 rows: 7 passes over
-    # the 77 MB weight instead of 8) and still fit the LDS (K <= 768).  Opt-in: measured 1 % slower
-    # at 1024 queries (704.8 / 707.9 vs 713.3 / 711.0 k tok/s, profiles/r3_sweep_lmhead_mt.jsonl)
-    fits5 = 80 * (kc * 2 + 32) + 8 * 4096 <= PS_LDS_BYTES
-    want = int(os.environ.get("DLMS_PS_MT", "4"))
-    if epi == EPI_ARGMAX and mt == 4 and want == 5 and fits5 and -(-M // 80) < -(-M // 64):
-        mt = 5
+    # (80-row LM-head panels, 7 passes over the 77 MB weight at 512 rows instead of 8, measured 1 %
+    # slower at 1024 queries: profiles/r3_sweep_lmhead_mt.jsonl)
     nt = 2
     row_blocks = -(-M // (16 * mt))
     tiles = N // (16 * nt)

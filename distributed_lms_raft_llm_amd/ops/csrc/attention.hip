@@ -337,21 +337,12 @@ extern "C" hipError_t dlms_attention_persist(const void* q, int ldq, const void*
                                              hipStream_t stream) {
     if (R <= 0 || H <= 0 || t_max <= 0 || blocks <= 0) return hipErrorInvalidValue;
     const int need = (R * H + 3) / 4;
-    static int blk = -1;  // DLMS_ATTN_BLK=0 restores the per-key softmax update
-    if (blk < 0) {
-        const char* e = getenv("DLMS_ATTN_BLK");
-        blk = (e != nullptr && e[0] == '0') ? 0 : 1;
-    }
-    auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(blocks < need ? blocks : need), dim3(256), 0, stream,
-                           reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
-                           reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, reinterpret_cast<bf16_t*>(out),
-                           ldo, R, H, t_max, n_slots, scale * 1.4426950408889634f);
-    };
-    if (blk)
-        launch(attn_persist_kernel<8, true>);
-    else
-        launch(attn_persist_kernel<8, false>);
+    // (the per-key softmax update measured the same at 1024 queries: 710/717 vs 715/710 k tok/s,
+    // profiles/r4_attn_blk_ab.jsonl -- the kernel is bound by the KV stream; the block-wise one stays)
+    hipLaunchKernelGGL((attn_persist_kernel<8, true>), dim3(blocks < need ? blocks : need), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
+                       reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, reinterpret_cast<bf16_t*>(out),
+                       ldo, R, H, t_max, n_slots, scale * 1.4426950408889634f);
     return hipGetLastError();
 }
 

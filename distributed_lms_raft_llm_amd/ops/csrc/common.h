@@ -299,9 +299,21 @@ struct GemmEpi {
     const float* a_scale;
     const float* w_scale;
     int n_slots;  // EPI_QKV: KV-cache slots (the checked build range-checks row_slot against it)
-    // EPI_F32X2: bf16 copy of the f32 output; EPI_GELU_LN: c1 = row sums of gamma (.) W, LN epsilon
+    // EPI_RESID_LN: bf16 copy of the updated residual (the next GEMM's A operand)
     bf16_t* out2;
     int ldo2;
+    // LayerNorm folded into a GEMM (ln_fold, gemm.hip MODE_LNF): c1 = row sums of gamma (.) W, epsilon,
+    // per-row statistics as ln_nst (sum, sum of squares) pairs per row over 32-column slices of the
+    // ln_k-wide residual (written by an EPI_RESID_LN producer)
     const float* ln_c1;
     float ln_eps;
+    float* ln_stats;
+    int ln_nst;
+    int ln_k;
+    int ln_fold;
+    // EPI_RESID_LN split-K: slice partials [split][rows][ldws] written through to memory, one arrival
+    // counter per output tile (zero between launches: the last arriver resets it)
+    float* ws;
+    int ldws;
+    unsigned int* tile_cnt;
 };

@@ -279,15 +279,9 @@ extern "C" hipError_t dlms_quantize_rows_fp8(const void* a, int lda, void* q, in
     return hipGetLastError();
 }
 
-// rows (waves) per workgroup of add_layernorm_kernel: DLMS_LN_ROWS_PER_BLOCK (1 or 4)
-static int ln_rows_per_block() {
-    static int v = 0;
-    if (v == 0) {
-        const char* e = getenv("DLMS_LN_ROWS_PER_BLOCK");
-        v = (e != nullptr && e[0] == '4') ? 4 : 1;
-    }
-    return v;
-}
+// one row (wave) per workgroup of add_layernorm_kernel (4 rows per workgroup measured the same:
+// profiles/r2_sweep_ln_rows_per_block.jsonl)
+static int ln_rows_per_block() { return 1; }
 
 template <int NSPLIT>
 static void launch_add_ln(int nv4, dim3 grid, int rpb, hipStream_t stream, float* x, int ldx, const float* parts, int ldp,

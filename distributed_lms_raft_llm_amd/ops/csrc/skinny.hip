@@ -45,15 +45,8 @@ __device__ __forceinline__ bf16x8_t load_wfrag(const bf16x8_t* p) {
 
 // The batch-1 LM head streams 77 MB once per token: non-temporal loads keep it from evicting the
 // 12 layers' ~170 MB of weights out of the 256 MiB Infinity Cache (a cyclic 248 MB stream through
-// an LRU cache of about that size would otherwise miss on every layer).  DLMS_LM_NT=0 turns it off.
-static int lm_head_nt() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("DLMS_LM_NT");
-        v = (e == nullptr || e[0] != '0') ? 1 : 0;
-    }
-    return v;
-}
+// an LRU cache of about that size would otherwise miss on every layer).
+static int lm_head_nt() { return 1; }
 
 // A fragment of rows [16 mt, 16 mt + 16) at k-block kb from the LDS LayerNorm image
 __device__ __forceinline__ bf16x8_t lds_a_frag(const char* img, int row_bytes, int row, int kb, int g) {
