@@ -103,8 +103,6 @@ class _Rows:
     split_fixed: int | None = None  # pinned split-K (M-independent arithmetic: prefill_split)
     persist_attn: bool = False  # decode attention as the low-occupancy persistent kernel
     pidx: int = 0  # index of the row part (timing-only experiments address parts by it)
-    stats: torch.Tensor | None = None  # LN-folded step: row statistics [M, d/32, 2] of the residual
-    cnt: torch.Tensor | None = None  # ... and this part's split-K tile tickets
 
 
 class HostResult:
@@ -247,20 +245,9 @@ class HipGPT2Engine:
         self.persist_attn_blocks = int(os.environ.get("DLMS_PERSIST_ATTN_BLOCKS", "768"))
         # (measured and removed: a skinny MFMA LM head at B <= 8, neutral at batch 1, and ln_f fused
         # into it, 37.3 vs 35.9 ms per query -- profiles/r2_lm_head_b1.txt)
-        # overlapped step (the 1024-query headline), TP=1 bf16: LayerNorms folded into the GEMMs.  The
-        # out-projection and c_proj update the residual in place (EPI_RESID_LN: split-K slices reduced
-        # in the kernel by the last arriving slice), leave a bf16 copy and per-row statistics; c_fc and
-        # the next layer's QKV apply LN2 / LN1 algebraically in their epilogues (ops.fold_ln_weights):
-        # 23 of the 25 add+LayerNorm launches per row half and step are gone.  DLMS_LN_FOLD=0: off.
-        fold_env = os.environ.get("DLMS_LN_FOLD", "0")
-        self.ln_fold = (self.tp_size == 1 and not self.w.fp8 and self.overlap and cfg.n_embd % ops.LN_SLICE == 0
-                        and cfg.n_embd // ops.LN_SLICE <= ops.LNF_MAX_SLOTS and fold_env != "0")
-        self.ln_fold_mode = fold_env  # EXPERIMENT: "1" both LNs, "2" LN2 only (out-proj unsplit), "3" LN2 only split 2
-        self._fold_qkv = self._fold_fc = None
-        if self.ln_fold:
-            L = self.w.layers
-            self._fold_qkv = [None] + [ops.fold_ln_weights(lw.ln1_g, lw.ln1_b, lw.w_qkv, lw.b_qkv) for lw in L[1:]]
-            self._fold_fc = [ops.fold_ln_weights(lw.ln2_g, lw.ln2_b, lw.w_fc, lw.b_fc) for lw in L]
+        # (measured and removed in round 5: the LayerNorms of the overlapped step folded into the GEMMs --
+        # residual projections reducing their split-K slices in-kernel, QKV / c_fc applying the LN
+        # algebraically -- 632-703 vs 718-721 k tok/s, profiles/r5_ln_fold_ab.jsonl; commit 9235466)
         # (measured and removed: 16-32 rows as latency-path parts on several HIP streams, slower than
         # the tiled step -- profiles/r2_sweep_small_overlap.jsonl)
         self.prefill_graphs = os.environ.get("DLMS_PREFILL_GRAPH", "1") != "0"
@@ -270,7 +257,10 @@ class HipGPT2Engine:
             raise ValueError("overlap_parts: 2, 3 or 4 (one hardware queue each)")
         if latency_path is None:
             latency_path = os.environ.get("DLMS_LATENCY_PATH", "1") != "0"
-        self.small_max = ops.skinny_addln_max_rows(cfg.n_embd) if (latency_path and not self.w.fp8) else 0
+        # (fp8 engines too: the latency path runs the bf16 weights the fp8 engine keeps beside its e4m3
+        # copies -- at <= 8 rows the decode is bound by launch and dependency latency, not weight bytes;
+        # W8A8 serves the prefill and the larger batches, where the weight stream matters)
+        self.small_max = ops.skinny_addln_max_rows(cfg.n_embd) if latency_path else 0
         inplace_ok = self.tp_size == 1 and os.environ.get("DLMS_SMALL_INPLACE", "1") != "0"
         if self.tp_size == 1 and not inplace_ok and \
                 any((k // 64) % self.SMALL_SPLIT for k in (self.w.d_local, self.w.ffn_local)):
@@ -295,8 +285,10 @@ class HipGPT2Engine:
         # attention fused with the out-projection for <= 4 rows (one launch fewer per layer); its
         # workgroups recompute a head's attention, so only for short caches
         # (TP=1: its per-head slabs are summed by the next fused add+LN kernel, 12 or 16 of them)
+        # (GPT-2-large / XL's 20 / 25 heads: only the head-grouped batch-1 kernel, groups of 5)
         self.fuse_ao = (self.small_max > 0 and self.tp_size == 1 and self.max_length <= 512 and
-                        self.w.n_heads_local in (12, 16) and cfg.n_embd <= 1024 and
+                        (self.w.n_heads_local in (12, 16) and cfg.n_embd <= 1024 or
+                         self.w.n_heads_local in (20, 25) and cfg.n_embd in (1280, 1600)) and
                         os.environ.get("DLMS_FUSE_ATTN_OPROJ", "1") != "0")
         if self.fuse_ao:
             try:
@@ -310,10 +302,15 @@ class HipGPT2Engine:
                     lw.w_o_sh = ops.shuffle_weight(lw.w_o)
             self.ao_parts = torch.zeros(self.w.n_heads_local, 4, cfg.n_embd, dtype=torch.float32, device=self.device)
         # batch 1: head groups of H/4 (3 or 4 heads) -> 4 slabs, 3 W_o tiles per workgroup
-        # (profiles/r2_attn_oproj_ab.txt: 36.6 vs 37.1 ms per query with one slab per head)
+        # (profiles/r2_attn_oproj_ab.txt: 36.6 vs 37.1 ms per query with one slab per head); GPT-2-large /
+        # XL: groups of 5 heads -> 4 / 5 slabs, 5 W_o tiles per workgroup (64 / 100 workgroups)
         Hl = self.w.n_heads_local
-        self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4)) else 0
-        self.ao_group_tiles = 3 if (cfg.n_embd // 16) % 3 == 0 else 1
+        if self.fuse_ao and Hl in (20, 25):
+            self.ao_groups, self.ao_group_tiles = 5, 5
+        else:
+            self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4)) else 0
+            self.ao_group_tiles = 3 if (cfg.n_embd // 16) % 3 == 0 else 1
+        self.ao_slabs = Hl // self.ao_groups if self.ao_groups else 0
         # batch 1 (TP=1, head-grouped attention): LN2 -> c_fc -> GELU -> c_proj as ONE kernel whose
         # workgroups add their 16-column slices into an int64 fixed-point residual (order-independent
         # integer atomics; ops.skinny_mlp) -- one launch and one dependent round trip fewer per layer
@@ -334,7 +331,7 @@ class HipGPT2Engine:
         # accumulator; rank 0 also adds the residual + b_p] -> integer xGMI all-reduce, which IS the
         # next residual on every rank (exact, order-independent) -- against eight launch-per-op
         # kernels (separate c_fc and c_proj, two split partial slabs to sum).  DLMS_TP_FUSED=0: off.
-        self.tp_fused = (self.tp_size > 1 and self.small_max > 0 and not self.w.fp8 and
+        self.tp_fused = (self.tp_size > 1 and self.small_max > 0 and
                          cfg.n_embd in ops.SKINNY_MLP_WIDTHS and self.w.ffn_local % 16 == 0 and
                          os.environ.get("DLMS_TP_FUSED", "1") != "0")
         self.tp_fused_steps = 0
@@ -407,9 +404,6 @@ class HipGPT2Engine:
         # cross-workgroup split attention (few rows, long caches): partials + arrival counters
         self.attn_ws = ops.AttnSplitWorkspace(self.SPLIT_ATTN_MAX_PAIRS, 2, dev)
         self.parts = torch.zeros(8, B, D, dtype=f32, device=dev)  # split-K / TP partial slabs
-        if self.ln_fold:  # LN-folded overlapped step: row statistics and per-part split-K tile tickets
-            self.ln_stats = torch.zeros(B, D // ops.LN_SLICE, 2, dtype=f32, device=dev)
-            self.tile_cnt = torch.zeros(self.overlap_parts, -(-B // 64) * (D // 64), dtype=torch.int32, device=dev)
         self.h = torch.zeros(B, D, dtype=bf, device=dev)
         self.q = torch.zeros(B, Dl, dtype=bf, device=dev)
         self.att = torch.zeros(B, Dl, dtype=bf, device=dev)
@@ -520,8 +514,9 @@ class HipGPT2Engine:
     def _rows(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
               h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None,
               tiles: "ops.AttnTiles | None" = None) -> "_Rows":
-        """Bundle the activation buffers of one row range for the per-layer phase functions."""
-        fp8 = self.w.fp8
+        """Bundle the activation buffers of one row range for the per-layer phase functions (fp8
+        engines: the e4m3 LayerNorm outputs when ``h8`` is given -- the latency path runs bf16)."""
+        fp8 = self.w.fp8 and h8 is not None
         r = _Rows(x=x[:M], parts=parts, h=h[:M], q=q[:M], att=att[:M], ff=ff[:M], row_slot=row_slot,
                   row_pos=row_pos, row_kvlen=row_kvlen, M=M, h8=h8[:M] if fp8 else None,
                   hsc=hsc[:M] if fp8 else None, tiles=tiles)
@@ -662,14 +657,10 @@ class HipGPT2Engine:
         r.split_cap = self.overlap_split_cap
         r.persist_attn = self.persist_attn_blocks > 0
         r.pidx = lo // max(1, hi - lo)
-        if self.ln_fold:
-            r.stats, r.cnt = self.ln_stats[lo:hi], self.tile_cnt[r.pidx]
         return r
 
     def _part_step(self, r: "_Rows", lo: int, penalty: float):
         """The whole decode step for one row range (rows are independent sequences)."""
-        if self.ln_fold and r.stats is not None and not self._skip(r):
-            return self._part_step_folded(r, lo, penalty)
         for li in range(len(self.w.layers)):
             self._attn_in(r, li)
             self._attn(r, li)
@@ -679,52 +670,6 @@ class HipGPT2Engine:
             self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
         else:
             self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
-
-    def _fold_split(self, K: int, want: int) -> int:
-        return max(d for d in range(1, want + 1) if (K // 64) % d == 0)
-
-    def _part_step_folded(self, r: "_Rows", lo: int, penalty: float):
-        """One row range's decode step with the LayerNorms folded into the GEMMs: per layer
-        QKV (LN1 in its epilogue; layer 0: a standalone LN1 of the embedding rows) -> attention ->
-        out-projection updating x in place (+ bf16 copy + row statistics) -> c_fc + GELU (LN2 in
-        its epilogue) -> c_proj updating x in place; then ln_f and the LM head.  Five launches per
-        layer instead of seven; the split-K slices of the two residual projections are reduced by
-        their last arriving slice (gemm.hip EPI_RESID_LN)."""
-        eps, D = self.cfg.layer_norm_epsilon, self.cfg.n_embd
-        so, sp = self._fold_split(self.w.d_local, 2), self._fold_split(self.w.ffn_local, 4)
-        mode = self.ln_fold_mode
-        if mode == "2":
-            so = 1
-        for li, lw in enumerate(self.w.layers):
-            kc, vc = self.kv[li, 0], self.kv[li, 1]
-            if mode in ("2", "3"):
-                ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, parts=r.pend[0], nsplit=r.pend[1], bias=r.pend[2],
-                                  out_bf16=r.h)
-                ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
-                         row_slot=r.row_slot, row_pos=r.row_pos)
-            elif li == 0:
-                ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, out_bf16=r.h)
-                ops.gemm(r.h, lw.w_qkv, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
-                         row_slot=r.row_slot, row_pos=r.row_pos)
-            else:
-                wq, c1, c2 = self._fold_qkv[li]
-                ops.gemm(r.h, wq, ops.EPI_QKV, bias=c2, ln_c1=c1, ln_eps=eps, ln_stats=r.stats, q_out=r.q,
-                         k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
-            self._attn(r, li)
-            ops.gemm(r.att, lw.w_o, ops.EPI_RESID_LN, bias=lw.b_o, resid=r.x, out=r.x, out2=r.h, ln_stats=r.stats,
-                     split_k=so, ws=r.parts, tile_cnt=r.cnt)
-            wf, c1, c2 = self._fold_fc[li]
-            ops.gemm(r.h, wf, ops.EPI_GELU_TANH, bias=c2, ln_c1=c1, ln_eps=eps, ln_stats=r.stats, out=r.ff)
-            if mode in ("2", "3"):
-                r.pend = self._row_parallel(r.ff, lw.w_p, lw.b_p, r.parts, r.M, r.split_cap, r.split_fixed)
-            else:
-                ops.gemm(r.ff, lw.w_p, ops.EPI_RESID_LN, bias=lw.b_p, resid=r.x, out=r.x, out2=r.h, ln_stats=r.stats,
-                         split_k=sp, ws=r.parts, tile_cnt=r.cnt)
-        if mode in ("2", "3"):
-            self._final_ln(r, r.h)
-        else:
-            ops.add_layernorm(r.x, self.w.lnf_g, self.w.lnf_b, eps, out_bf16=r.h)
-        self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
 
     def _decode_step_overlap(self, B: int, penalty: float, nsteps: int = 1):
         """Decode step as ``overlap_parts`` row ranges on as many HIP streams (one hardware queue
@@ -864,12 +809,12 @@ class HipGPT2Engine:
                                       parts=parts, nsplit=pend[0], res_bias=pend[1], bias=lw.b_qkv, q_out=r.q,
                                       k_cache=kc, v_cache=vc, row_slot=r.row_slot, row_pos=r.row_pos)
                 cur = 1 - cur
-            if self.fuse_ao and B == 1 and self.ao_groups:
+            if self.fuse_ao and B == 1 and self.ao_groups and self.ao_slabs == 4:
                 # heads in groups of H/4: exactly the 4 slabs the fused add+LN sums cheaply
                 ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
                                             self.ao_groups, tiles=self.ao_group_tiles)
                 mlp_parts, ns, rb = self.ao_parts[:4, :1], 4, lw.b_o
-            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS:
+            elif self.fuse_ao and B <= self.FUSE_AO_MAX_ROWS and self.w.n_heads_local in (12, 16):
                 ops.attention_oproj(self.q[:B], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts)
                 mlp_parts, ns, rb = self.ao_parts[:, :B], self.w.n_heads_local, lw.b_o
             elif inplace:
@@ -902,8 +847,8 @@ class HipGPT2Engine:
     def _decode_layers_fused_mlp(self, r, B: int):
         """Layers as [LN1 + QKV (+ clear the MLP's accumulator)] -> attention + out-projection ->
         [add + LN2 + c_fc + GELU + c_proj, added into the int64 fixed-point residual xr[l % 2]].
-        Batch 1 with head groups (12 / 16 heads): attention fused with the out-projection (4 head-group
-        slabs the MLP sums); otherwise split attention, then the skinny out-projection adding into the residual in place (the
+        Batch 1 with head groups (12 / 16 / 20 / 25 heads): attention fused with the out-projection (4 or
+        5 head-group slabs the MLP sums); otherwise split attention, then the skinny out-projection adding into the residual in place (the
         f32 embedding rows x in layer 0, copy 0 of the fixed-point residual after that).  The final
         residual is xr[(L - 1) % 2]."""
         eps = self.cfg.layer_norm_epsilon
@@ -917,8 +862,9 @@ class HipGPT2Engine:
             if B == 1 and self.ao_groups:
                 ops.attention_oproj_grouped(self.q[:1], kc, vc, r.row_slot, r.row_kvlen, lw.w_o_sh, self.ao_parts,
                                             self.ao_groups, tiles=self.ao_group_tiles)
+                ns = self.ao_slabs
                 ops.skinny_mlp(xin, lw.ln2_g, lw.ln2_b, eps, lw.w_fc_sh, lw.b_fc, lw.w_p_sl, lw.b_p, acc,
-                               parts=self.ao_parts[:4, :1], nsplit=4, res_bias=lw.b_o)
+                               parts=self.ao_parts[:ns, :1], nsplit=ns, res_bias=lw.b_o)
             else:
                 self._attn(r, li)
                 ops.skinny_gemm(self.att[:B], lw.w_o_sh, ops.EPI_F32, bias=lw.b_o, out=xin if li == 0 else xin[0])

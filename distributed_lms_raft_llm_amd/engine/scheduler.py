@@ -82,10 +82,20 @@ class _Req:
     steps_left: int = 0  # decode steps until max_length (an upper bound: EOS may come first)
 
 
+class Overloaded(RuntimeError):
+    """``submit`` refused a query: the admission queue already holds ``max_queue`` queries (the
+    servers answer RESOURCE_EXHAUSTED at once, so an overloaded replica sheds load in
+    microseconds instead of queueing queries until their client deadlines expire)."""
+
+
 class ContinuousBatcher:
     def __init__(self, engine, repetition_penalty: float = 1.2, chunk: int = 8, max_admit: int | None = None,
-                 name: str = "tutor", stream_priority: int | None = None):
+                 name: str = "tutor", stream_priority: int | None = None, max_queue: int = 0):
+        """``max_queue``: queries allowed to wait for a free KV slot before ``submit`` raises
+        ``Overloaded`` (0 = unbounded; the tutoring servers default to one batch of slots)."""
         self.engine = engine
+        self.max_queue = int(max_queue or 0)
+        self.rejected = 0
         env_prio = os.environ.get("DLMS_BATCHER_STREAM_PRIORITY")
         self.stream_priority = int(env_prio) if env_prio else stream_priority
         self.penalty = float(repetition_penalty)
@@ -117,6 +127,10 @@ class ContinuousBatcher:
                 raise RuntimeError("batcher stopped")
             if self._error is not None:
                 raise RuntimeError("batcher failed") from self._error
+            if self.max_queue and len(self._queue) >= self.max_queue:
+                self.rejected += 1
+                METRICS.inc(f"{self.name}_rejected_total")
+                raise Overloaded(f"{len(self._queue)} queries already waiting for a KV slot")
             self._queue.append(_Req(p, fut))
             self._cv.notify()
         return fut

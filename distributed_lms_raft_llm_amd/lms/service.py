@@ -59,6 +59,7 @@ MSG_LLM_IRRELEVANT = ("Your query does not relate to your assignment. "
                       "Please ask a question related to your assignment.")
 MSG_UNAVAILABLE = "The LMS cluster is unavailable (no leader). Please retry."
 MSG_TUTOR_UNAVAILABLE = "The tutoring service is unavailable. Please retry later."
+MSG_TUTOR_BUSY = "The tutoring service is busy. Please retry in a moment."
 
 
 class TutoringClient:
@@ -69,6 +70,9 @@ class TutoringClient:
     The reference has one module-level channel to a hard-coded address (``lms_server.py:39-40``)."""
 
     RETRY_CODES = (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.CANCELLED)
+    # an overloaded replica refuses at once (its admission queue is full): try the others, but it
+    # is healthy -- not marked down
+    BUSY_CODES = (grpc.StatusCode.RESOURCE_EXHAUSTED,)
 
     def __init__(self, address, timeout: float = 120.0, down_s: float = 2.0, aio_connections: int = 4):
         addrs = address.split(",") if isinstance(address, str) else list(address)
@@ -103,6 +107,9 @@ class TutoringClient:
                 return self._stubs[i].GetLLMAnswer(pb.QueryRequest(token=token, query=query), timeout=self.timeout)
             except grpc.RpcError as e:
                 last = e
+                if e.code() in self.BUSY_CODES:
+                    METRICS.inc("tutor_busy_total")
+                    continue
                 if e.code() not in self.RETRY_CODES:
                     raise
                 METRICS.inc("tutor_failover_total")
@@ -134,6 +141,9 @@ class TutoringClient:
                 return await stub.GetLLMAnswer(pb.QueryRequest(token=token, query=query), timeout=self.timeout)
             except grpc.RpcError as e:
                 last = e
+                if e.code() in self.BUSY_CODES:
+                    METRICS.inc("tutor_busy_total")
+                    continue
                 if e.code() not in self.RETRY_CODES:
                     raise
                 METRICS.inc("tutor_failover_total")
@@ -157,6 +167,16 @@ class TutoringClient:
 
 
 _SLOW = object()  # _llm_prelude_fast: "run the full prelude on the worker pool"
+
+
+def _tutor_error_message(e: grpc.RpcError) -> str:
+    """What the student sees when the tutoring tier fails: every replica refusing for load is
+    "busy" (retry soon), anything else "unavailable"."""
+    code = e.code() if hasattr(e, "code") else None
+    if code == grpc.StatusCode.RESOURCE_EXHAUSTED:
+        METRICS.inc("llm_answer_busy_total")
+        return MSG_TUTOR_BUSY
+    return MSG_TUTOR_UNAVAILABLE
 
 
 class LMSServicer:
@@ -510,7 +530,7 @@ class LMSServicer:
             resp = self.tutor.ask(request.token, request.query)
         except grpc.RpcError as e:
             log.warning("tutoring call failed: %s", e.code())
-            return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+            return pb.QueryResponse(success=True, response=_tutor_error_message(e))
         self._llm_done(t0, tt)
         return resp
 
@@ -538,7 +558,7 @@ class LMSServicer:
             resp = await self.tutor.ask_async(request.token, request.query)
         except grpc.RpcError as e:
             log.warning("tutoring call failed: %s", e.code())
-            return pb.QueryResponse(success=True, response=MSG_TUTOR_UNAVAILABLE)
+            return pb.QueryResponse(success=True, response=_tutor_error_message(e))
         self._llm_done(t0, tt)
         return resp
 

@@ -35,9 +35,7 @@ SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "en
            "dataflow.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
-EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL, EPI_RESID_LN = range(8)
-LN_SLICE = 32        # columns per LayerNorm-statistics slot (gemm.hip EPI_RESID_LN -> MODE_LNF)
-LNF_MAX_SLOTS = 32   # a folded consumer reads at most this many slots per row (d <= 1024)
+EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
 
 _lock = threading.Lock()
 _lib = None
@@ -120,9 +118,6 @@ class GemmEpi(ctypes.Structure):
         ("split_k", ctypes.c_int), ("split_stride", ctypes.c_longlong),
         ("a_scale", ctypes.c_void_p), ("w_scale", ctypes.c_void_p),
         ("n_slots", ctypes.c_int),
-        ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int), ("ln_c1", ctypes.c_void_p), ("ln_eps", ctypes.c_float),
-        ("ln_stats", ctypes.c_void_p), ("ln_nst", ctypes.c_int), ("ln_k", ctypes.c_int), ("ln_fold", ctypes.c_int),
-        ("ws", ctypes.c_void_p), ("ldws", ctypes.c_int), ("tile_cnt", ctypes.c_void_p),
     ]
 
 
@@ -199,11 +194,7 @@ def _bind(L):
     L.dlms_gemm_force_tile.restype = None
     L.dlms_gemm_tile_count.argtypes = [ctypes.c_int, ctypes.c_int]
     L.dlms_gemm_tile_count.restype = ctypes.c_long
-    L.dlms_attention_variant.argtypes = [ctypes.c_int]
-    L.dlms_attention_variant.restype = None
     # in-situ tuning knobs (tests and production leave them unset)
-    if os.environ.get("DLMS_ATTN_VARIANT"):
-        L.dlms_attention_variant(int(os.environ["DLMS_ATTN_VARIANT"]))
     if os.environ.get("DLMS_GEMM_TILE"):
         L.dlms_gemm_force_tile(int(os.environ["DLMS_GEMM_TILE"]))
     L.dlms_error_string.argtypes = [ctypes.c_int]
@@ -302,20 +293,10 @@ def _req(t: torch.Tensor, dtype, name: str, dim: int | None = None):
 def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, out=None, resid=None,
          q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
          argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0,
-         split_k: int = 1, a_scale=None, w_scale=None, out2=None, ln_c1=None, ln_eps: float = 1e-5,
-         ln_stats=None, ws=None, tile_cnt=None):
+         split_k: int = 1, a_scale=None, w_scale=None):
     """C = a @ w.T with a fused epilogue.  a: bf16 [M, K]; w: bf16 [N, K] (N % 64 == 0, K % 64 == 0).
     fp8 (W8A8): a and w ``torch.float8_e4m3fn`` with f32 ``a_scale`` [M] and ``w_scale`` [N]
-    (C = diag(a_scale) (a @ w.T) diag(w_scale)); K % 128 == 0.
-
-    ``EPI_RESID_LN`` (residual projection of the LayerNorm-folded decode chain): ``out`` (f32
-    [M, N], normally the residual ``resid`` itself) = resid + a w^T + bias, ``out2`` = its bf16
-    copy, ``ln_stats`` (f32 [M, >= N/32, 2]) = each row's (sum, sum of squares) per 32 columns;
-    ``split_k`` > 1 needs ``ws`` (f32 [>= split_k, M, N] slice partials) and ``tile_cnt`` (int32,
-    zero, one per output tile: the kernel leaves it zero).
-    ``ln_stats`` with EPI_QKV / EPI_GELU_TANH / EPI_BF16 (and ``ln_c1``): LayerNorm folded in --
-    ``a`` is the raw bf16 residual, ``w``/``ln_c1``/``bias`` the ``fold_ln_weights`` triple, the
-    row statistics those of an EPI_RESID_LN producer over K columns."""
+    (C = diag(a_scale) (a @ w.T) diag(w_scale)); K % 128 == 0."""
     fp8 = a.dtype == FP8
     _req(a, FP8 if fp8 else torch.bfloat16, "a", 2)
     _req(w, FP8 if fp8 else torch.bfloat16, "w", 2)
@@ -336,51 +317,6 @@ def gemm(a: torch.Tensor, w: torch.Tensor, epi: int = EPI_BF16, *, bias=None, ou
         if bias.numel() < N:
             raise ValueError("bias too short")
         ep.bias = bias.data_ptr()
-    if epi == EPI_RESID_LN:
-        if fp8:
-            raise ValueError("EPI_RESID_LN: bf16 inputs only")
-        if N % LN_SLICE:
-            raise ValueError(f"EPI_RESID_LN: N % {LN_SLICE}")
-        _req(out, torch.float32, "out", 2)
-        _req(resid, torch.float32, "resid", 2)
-        _req(out2, torch.bfloat16, "out2", 2)
-        _req(ln_stats, torch.float32, "ln_stats", 3)
-        if out.shape[0] < M or out.shape[1] < N or resid.shape[0] < M or resid.shape[1] < N or \
-                out2.shape[0] < M or out2.shape[1] < N or ln_stats.shape[0] < M or ln_stats.shape[1] * LN_SLICE < N \
-                or ln_stats.shape[2] != 2 or not ln_stats.is_contiguous():
-            raise ValueError("EPI_RESID_LN buffers too small")
-        for t in (out, resid, out2):
-            if t.data_ptr() % 16 or t.stride(0) % 8:
-                raise ValueError("EPI_RESID_LN: rows must be 16-byte aligned")
-        if split_k < 1 or K % (64 * split_k):
-            raise ValueError(f"split_k={split_k} must divide K/64 (K={K})")
-        ep.out, ep.ldo, ep.resid, ep.ldr = out.data_ptr(), out.stride(0), resid.data_ptr(), resid.stride(0)
-        ep.out2, ep.ldo2 = out2.data_ptr(), out2.stride(0)
-        ep.ln_stats, ep.ln_nst = ln_stats.data_ptr(), ln_stats.shape[1]
-        ep.split_k = split_k
-        if split_k > 1:
-            _req(ws, torch.float32, "ws", 3)
-            _req(tile_cnt, torch.int32, "tile_cnt", 1)
-            tiles = -(-M // 64) * (N // 64)
-            if ws.shape[0] < split_k or ws.shape[1] < M or ws.shape[2] < N or ws.stride(1) % 4 or ws.data_ptr() % 16 \
-                    or tile_cnt.numel() < tiles or ws.stride(0) * split_k * 4 >= 2 ** 31:
-                raise ValueError("EPI_RESID_LN: split-K workspace / tile counters too small")
-            ep.ws, ep.ldws, ep.split_stride, ep.tile_cnt = ws.data_ptr(), ws.stride(1), ws.stride(0), tile_cnt.data_ptr()
-        _check(lib().dlms_gemm(epi, _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, ctypes.byref(ep), _stream()),
-               "dlms_gemm")
-        return out
-    if ln_stats is not None:
-        if fp8 or epi not in (EPI_QKV, EPI_GELU_TANH, EPI_BF16):
-            raise ValueError("folded LayerNorm: bf16 QKV / GELU / bf16 epilogues only")
-        _req(ln_stats, torch.float32, "ln_stats", 3)
-        _req(ln_c1, torch.float32, "ln_c1", 1)
-        nst = ln_stats.shape[1]
-        if ln_stats.shape[0] < M or nst * LN_SLICE != K or nst > LNF_MAX_SLOTS or ln_c1.numel() < N or \
-                not ln_stats.is_contiguous() or ln_stats.shape[2] != 2:
-            raise ValueError(f"folded LayerNorm: statistics [M, K/{LN_SLICE}, 2] (K <= {LN_SLICE * LNF_MAX_SLOTS}) "
-                             f"and c1 [N] needed")
-        ep.ln_stats, ep.ln_nst, ep.ln_k, ep.ln_fold = ln_stats.data_ptr(), nst, K, 1
-        ep.ln_c1, ep.ln_eps = ln_c1.data_ptr(), float(ln_eps)
     if epi in (EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32):
         want = torch.float32 if epi == EPI_F32 else torch.bfloat16
         if out is None:
@@ -774,19 +710,6 @@ def cosine(a: torch.Tensor, b: torch.Tensor, eps: float = 1e-8, out=None):
 SKINNY_MAX_M = 32
 
 
-def fold_ln_weights(gamma: torch.Tensor, beta: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None):
-    """LayerNorm folded into the following GEMM (``gemm(..., ln_stats=...)``): LN(x) W^T + b = rstd (x W'^T - mu c1)
-    + c2 with W' = bf16(gamma (.) W) (the operand the MFMAs see), c1 = row sums of that bf16 W' in
-    fp32, c2 = beta W^T + b.  w: bf16 [N, K]; gamma, beta: f32 [K].  Returns (W', c1, c2)."""
-    wf = w.float()
-    wp = (wf * gamma.float()[None, :]).to(torch.bfloat16)
-    c1 = wp.float().sum(dim=1).contiguous()
-    c2 = wf @ beta.float()
-    if b is not None:
-        c2 = c2 + b.float()
-    return wp.contiguous(), c1, c2.contiguous()
-
-
 def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
     """[N, K] bf16 (K contiguous) -> MFMA B-fragment order [N/16, K/32, 64, 8]: lane l of the
     16x16x32 bf16 MFMA holds W[16 ng + (l & 15)][32 kb + 8 (l >> 4) + j] at [ng, kb, l, j], so one
@@ -1092,8 +1015,9 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
         _req(t, torch.float32, n, 1)
         if t.numel() != size:
             raise ValueError(f"skinny_mlp: {n} size")
-    if nsplit not in (0, 1, 4) or (nsplit == 4 and K > 1024):
-        raise ValueError("skinny_mlp: nsplit in {0, 1, 4} (4: d <= 1024)")
+    if nsplit not in (0, 1, 4, 5) or (nsplit == 4 and K > 1280) or (nsplit == 5 and K != 1600):
+        raise ValueError("skinny_mlp: nsplit in {0, 1, 4, 5} (4: d <= 1280 -- head groups of 3-5; 5: d 1600, "
+                         "GPT-2-XL's 25 heads in groups of 5)")
     ldp, sstride = 0, 0
     if nsplit:
         _req(parts, torch.float32, "parts", 3)
@@ -1260,8 +1184,9 @@ def attention_oproj(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
 def attention_oproj_grouped(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
                             row_kvlen: torch.Tensor, wo_sh: torch.Tensor, parts: torch.Tensor, heads_per_group: int,
                             scale: float | None = None, tiles: int = 3) -> torch.Tensor:
-    """``attention_oproj`` for ONE row with heads in groups of ``heads_per_group`` (3 or 4): group g's
-    share of the out-projection goes to ``parts[g, 0, :N]`` -- H / heads_per_group slabs."""
+    """``attention_oproj`` for ONE row with heads in groups of ``heads_per_group`` (3, 4 or 5): group
+    g's share of the out-projection goes to ``parts[g, 0, :N]`` -- H / heads_per_group slabs.
+    (Groups of 5 -- GPT-2-large / XL -- run 2 waves per head; ``tiles`` then in {4, 5, 10}.)"""
     _req(q, torch.bfloat16, "q", 2)
     _req(k_cache, torch.bfloat16, "k_cache", 4)
     _req(v_cache, torch.bfloat16, "v_cache", 4)
@@ -1276,8 +1201,10 @@ def attention_oproj_grouped(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
         raise ValueError("attention_oproj_grouped: one row")
     if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64 or wo_sh.shape[1] * 32 != H * 64:
         raise ValueError("attention_oproj_grouped: bad shapes")
-    if hg not in (3, 4) or H % hg or (N // 16) % tiles:
-        raise ValueError("attention_oproj_grouped: heads_per_group in {3, 4} dividing H, tiles dividing N/16")
+    ok_tiles = (4, 5, 10) if hg == 5 else (1, 2, 3, 4)
+    if hg not in (3, 4, 5) or H % hg or (N // 16) % tiles or tiles not in ok_tiles:
+        raise ValueError("attention_oproj_grouped: heads_per_group in {3, 4, 5} dividing H, tiles dividing N/16 "
+                         f"and in {ok_tiles}")
     if parts.shape[0] < H // hg or parts.shape[2] < N or parts.stride(2) != 1:
         raise ValueError("attention_oproj_grouped: parts must be [>= H/hg, >= 1, >= N]")
     sc = (1.0 / 8.0) if scale is None else scale

@@ -349,26 +349,16 @@ extern "C" hipError_t dlms_attention_persist(const void* q, int ldq, const void*
 // Default: 4-deep unroll with non-temporal K/V loads (the cache is streamed once per layer; keeping
 // it out of L2/MALL leaves them to the weights): +6 % whole-step at 1024 queries, +4.5 % at 256
 // (profiles/r1_attention_variants.log, in-situ A/B in profiles/r1_bench_lines.jsonl).
-// Tuning override: 0 = (unroll 4, nt), 1 = (8), 2 = (4, plain), 3 = (8, nt).
-static int g_attn_variant = 0;
-extern "C" void dlms_attention_variant(int v) { g_attn_variant = v; }
 
 extern "C" hipError_t dlms_attention(const void* q, int ldq, const void* kc, const void* vc, const int* row_slot,
                                      const int* row_kvlen, void* out, int ldo, int R, int H, int t_max, int n_slots,
                                      float scale, hipStream_t stream) {
     if (R <= 0 || H <= 0 || t_max <= 0) return hipErrorInvalidValue;
     const float scale_log2 = scale * 1.4426950408889634f;
-    auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((H + 3) / 4, R), dim3(256), 0, stream, reinterpret_cast<const bf16_t*>(q), ldq,
-                           reinterpret_cast<const bf16_t*>(kc), reinterpret_cast<const bf16_t*>(vc), row_slot,
-                           row_kvlen, reinterpret_cast<bf16_t*>(out), ldo, H, t_max, n_slots, scale_log2);
-    };
-    switch (g_attn_variant) {
-        case 1: launch(attn_wave_kernel<8, false>); break;
-        case 2: launch(attn_wave_kernel<4, false>); break;
-        case 3: launch(attn_wave_kernel<8, true>); break;
-        default: launch(attn_wave_kernel<4, true>); break;
-    }
+    hipLaunchKernelGGL((attn_wave_kernel<4, true>), dim3((H + 3) / 4, R), dim3(256), 0, stream,
+                       reinterpret_cast<const bf16_t*>(q), ldq, reinterpret_cast<const bf16_t*>(kc),
+                       reinterpret_cast<const bf16_t*>(vc), row_slot, row_kvlen, reinterpret_cast<bf16_t*>(out), ldo,
+                       H, t_max, n_slots, scale_log2);
     return hipGetLastError();
 }
 

@@ -73,11 +73,6 @@ __device__ __forceinline__ float xor_lane(float v, int o) {
 // partner lanes), otherwise x = own, y = partner (xor_lane).  Callers combine x and y symmetrically
 // (sums, the online-softmax merge), which gives the same result as (own, partner) bit for bit.
 __device__ __forceinline__ void lane_pair(float v, int o, float& x, float& y) {
-#if DLMS_NO_PERMLANE  // A/B builds: the ds_bpermute exchange for every o
-    x = v;
-    y = xor_lane(v, o);
-    return;
-#endif
     if (o == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
         x = __uint_as_float(r[0]);
@@ -134,19 +129,7 @@ __device__ __forceinline__ float lane_value(float v, int lane) {
 
 // Full-wave reductions: butterflies inside each 16-lane row by DPP, then the four row results
 // combined in a fixed order from scalar registers (the same value in every lane, deterministic).
-// (-DDLMS_SHFL_REDUCE=1 builds the former ds_bpermute butterflies, for A/B runs)
-#if DLMS_SHFL_REDUCE
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-#else
+// (the former ds_bpermute butterflies measured slower on every path: profiles/r2_sweep_dpp_reduce.jsonl)
 __device__ __forceinline__ float wave_sum(float v) {
     v += dpp_perm<0xB1>(v);
     v += dpp_perm<0x4E>(v);
@@ -162,7 +145,6 @@ __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_perm<0x140>(v));
     return fmaxf(fmaxf(lane_value(v, 0), lane_value(v, 16)), fmaxf(lane_value(v, 32), lane_value(v, 48)));
 }
-#endif
 
 __device__ __forceinline__ float gelu_tanh(float x) {
     const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
@@ -299,21 +281,4 @@ struct GemmEpi {
     const float* a_scale;
     const float* w_scale;
     int n_slots;  // EPI_QKV: KV-cache slots (the checked build range-checks row_slot against it)
-    // EPI_RESID_LN: bf16 copy of the updated residual (the next GEMM's A operand)
-    bf16_t* out2;
-    int ldo2;
-    // LayerNorm folded into a GEMM (ln_fold, gemm.hip MODE_LNF): c1 = row sums of gamma (.) W, epsilon,
-    // per-row statistics as ln_nst (sum, sum of squares) pairs per row over 32-column slices of the
-    // ln_k-wide residual (written by an EPI_RESID_LN producer)
-    const float* ln_c1;
-    float ln_eps;
-    float* ln_stats;
-    int ln_nst;
-    int ln_k;
-    int ln_fold;
-    // EPI_RESID_LN split-K: slice partials [split][rows][ldws] written through to memory, one arrival
-    // counter per output tile (zero between launches: the last arriver resets it)
-    float* ws;
-    int ldws;
-    unsigned int* tile_cnt;
 };

@@ -171,7 +171,7 @@ enum { C_READY = 0, C_ABORT = 2, C_DONE = 3, C_CONT = 4, C_GATHER = 5, C_LOADED 
 // C_GATHER: the comm wave is waiting on a hand-off (residual edge, q/k/v granules): the loaders
 // issue no new weight batches meanwhile, so the poll's loads do not queue behind this CU's own
 // refill burst (MI355X_MICROARCH.md "gather-pass": 1.0-1.7 us behind an unthrottled refill vs
-// 0.3-0.65 with the CU's own DMA quiet).  Args::gather_pause (DLMS_DF_GATHER_PAUSE=0: off, A/B).
+// 0.3-0.65 with the CU's own DMA quiet).  Args::gather_pause (always 1 from ops/dataflow.py).
 // (C_LOADED + j: loader wave j's completed-batch count)
 // row state words (st[b * 8 + k])
 enum { S_TOK = 0, S_POS = 1, S_FIN = 2, S_LEN = 3, S_SLOT = 4 };

@@ -20,18 +20,6 @@
 //   128-B LDS rows then hold 128 k-elements, each 16-B fragment feeds two
 //   v_mfma_f32_16x16x32_fp8_fp8, and acc is rescaled by a_scale[row] * w_scale[col] before the
 //   epilogue.  W8A8 halves the weight bytes the latency-bound decode GEMMs stream.)
-//   EPI_RESID_LN    x = x + acc + bias (in place), out2 = bf16(x), and LayerNorm statistics of the new
-//                   rows (sum, sum of squares per 32-column slice) for the next GEMM, which folds the
-//                   LayerNorm in (MODE_LNF below): the residual projections of the 512-row decode halves
-//                   without a standalone add+LayerNorm launch.  Split-K slices publish their partial
-//                   tiles write-through (sc1) and take an arrival ticket per output tile; the LAST
-//                   arriver sums the slices in slice order (deterministic whoever arrives last) --
-//                   no waiting, so no co-residency assumption (MI355X_MICROARCH.md "Valid forms",
-//                   first row of the hand-off table).
-//   MODE_LNF        (QKV / c_fc epilogues) LN(x) W^T + b = rstd (x W'^T - mu c1) + c2 with W' = bf16(gamma (.) W),
-//                   c1 = row sums of W', c2 = beta W^T + b (ops.fold_ln_weights); A = bf16(x) from the
-//                   producer and (mu, rstd) from its statistics, loaded in the prologue under the first
-//                   DMA: the main loop is unchanged
 //   EPI_PARTIAL     split-K: slice s stores its raw fp32 partial tile; the following fused
 //                   residual-add + LayerNorm kernel sums the slices in a fixed order (deterministic,
 //                   no atomics) -- the decode projections with N = d are split 2-4 ways so the
@@ -40,11 +28,8 @@
 #include <atomic>
 #include <stdlib.h>
 
-enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6,
-       EPI_RESID_LN = 7 };
-enum { MODE_REGPF = 1, MODE_GROUPED = 2, MODE_LNF = 4 };
-constexpr int LN_SLICE = 32;    // columns per LayerNorm-statistics slot (EPI_RESID_LN -> MODE_LNF)
-constexpr int LNF_MAX_SLOTS = 32;  // d <= 1024
+enum { EPI_BF16 = 0, EPI_GELU_TANH = 1, EPI_GELU_ERF = 2, EPI_F32 = 3, EPI_QKV = 4, EPI_ARGMAX = 5, EPI_PARTIAL = 6 };
+enum { MODE_REGPF = 1, MODE_GROUPED = 2 };
 
 // struct GemmEpi lives in common.h (shared with the ABI probe in api.hip)
 
@@ -76,7 +61,6 @@ __device__ __forceinline__ void wait_vmcnt() {
 //   bit 1  GROUPED: tiles enumerated in groups of GROUP_M row tiles x all column tiles, so the 32
 //          workgroups an XCD runs at once share 4 A panels and 8 W panels through its L2 (the
 //          column-major order gave every one of them its own A panel: 32 panels from beyond L2)
-//   bit 2  LNF: LayerNorm folded into the epilogue (see EPI_RESID_LN above)
 #define GROUP_M 4
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN, int MODE = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __restrict__ A, int lda,
@@ -109,18 +93,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 
     const int tiles_m = (M + BM - 1) / BM;
     const int nwg = gridDim.x;
-    const int nsplit = (EPI == EPI_PARTIAL || EPI == EPI_RESID_LN) ? ep.split_k : 1;
+    const int nsplit = EPI == EPI_PARTIAL ? ep.split_k : 1;
     const int tiles = nwg / nsplit;
     const int bid0 = xcd_remap(blockIdx.x, nwg);
     const int split = bid0 / tiles;
     const int bid = bid0 - split * tiles;
     constexpr bool REGPF = (MODE & MODE_REGPF) != 0;
     constexpr bool GROUPED = (MODE & MODE_GROUPED) != 0;
-    constexpr bool LNF = (MODE & MODE_LNF) != 0;
     static_assert(!REGPF || (STAGES == 2 && IN == IN_BF16), "REGPF: 2 bf16 stages");
-    static_assert(!LNF || ((EPI == EPI_QKV || EPI == EPI_GELU_TANH || EPI == EPI_BF16) && IN == IN_BF16 && BM * 4 <= NT),
-                  "LNF: bf16 QKV / c_fc epilogues, 4 threads per tile row");
-    static_assert(EPI != EPI_RESID_LN || (BN % LN_SLICE == 0 && IN == IN_BF16), "EPI_RESID_LN: 32-column slices");
     int tile_m, tile_n;
     if constexpr (GROUPED) {
         const int tiles_n = N / BN;
@@ -166,20 +146,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-    // LNF: (mean, rstd) per tile row from the producer's slice statistics -- 4 threads per row load
-    // their share of the slots here, before the ring prologue (so the compiler's wait for them lets
-    // the DMA stay in flight), and reduce them after it
-    __shared__ float2 ln_stat[LNF ? BM : 1];
-    float2 lnv[LNF ? LNF_MAX_SLOTS / 4 : 1];
-    if constexpr (LNF) {
-        const int lr = tid >> 2, q = tid & 3;
-        const int row = m0 + lr < M ? m0 + lr : M - 1;
-        const float2* st = reinterpret_cast<const float2*>(ep.ln_stats) + (size_t)row * ep.ln_nst;
-#pragma unroll
-        for (int k = 0; k < LNF_MAX_SLOTS / 4; ++k)
-            lnv[k] = (q + 4 * k < ep.ln_nst && lr < BM) ? st[q + 4 * k] : make_float2(0.f, 0.f);
-    }
 
     const int nk = k_len / BKE;
     const int frow = lane & 15;
@@ -230,25 +196,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 #pragma unroll
         for (int s = 0; s < STAGES - 1; ++s)
             if (s < nk) issue(s, s * BKE);
-    }
-    if constexpr (LNF) {
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int k = 0; k < LNF_MAX_SLOTS / 4; ++k) {
-            s1 += lnv[k].x;
-            s2 += lnv[k].y;
-        }
-        s1 += __shfl_xor(s1, 1);
-        s2 += __shfl_xor(s2, 1);
-        s1 += __shfl_xor(s1, 2);
-        s2 += __shfl_xor(s2, 2);
-        if ((tid & 3) == 0 && (tid >> 2) < BM) {
-            const float invk = 1.0f / (float)ep.ln_k;
-            const float mean = s1 * invk;
-            const float var = fmaxf(s2 * invk - mean * mean, 0.f);
-            ln_stat[tid >> 2] = make_float2(mean, rsqrtf(var + ep.ln_eps));
-        }
-        // (read after the staged epilogue's first __syncthreads)
     }
 
     for (int kt = 0; kt < (REGPF ? 0 : nk); ++kt) {
@@ -394,101 +341,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
         return;
     }
 
-    if constexpr (EPI == EPI_RESID_LN) {
-        // (1) the fp32 tile into LDS; (2) split-K: publish it write-through, take the tile's ticket,
-        // only the last arriver goes on; (3) x_new = (sum of slices in slice order + bias) + x, stored
-        // f32 (in place) and bf16; (4) per-row (sum, sum of squares) of each 32-column slice
-        constexpr int SROW = BN * 4 + 16;
-        constexpr int CPR = BN / 4;  // 16-B chunks per tile row
-        __shared__ int s_last;
-        __syncthreads();  // every wave is done reading the last ring stage
-        {
-            const int lrow0 = wm * WTM + (lane >> 4) * 4;
-            const int lcol0 = wn * WTN + (lane & 15);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        *reinterpret_cast<float*>(smem + (lrow0 + i * 16 + r) * SROW + (lcol0 + j * 16) * 4) =
-                            acc[i][j][r];
-        }
-        __syncthreads();
-        const int S = ep.split_k;
-        const auto wsr = __builtin_amdgcn_make_buffer_rsrc(ep.ws, (short)0, 0x7fffffff, 0x00020000);
-        if (S > 1) {
-            for (int c = tid; c < BM * CPR; c += NT) {
-                const int lr = c / CPR, ch = c - lr * CPR;
-                const int row = m0 + lr;
-                if (row >= M) continue;
-                const u32x4_t val = *reinterpret_cast<const u32x4_t*>(smem + lr * SROW + ch * 16);
-                const long long off = ((long long)split * ep.split_stride + (long long)row * ep.ldws + n0 + ch * 4) * 4;
-                __builtin_amdgcn_raw_buffer_store_b128(val, wsr, (int)off, 0, 16 /* sc1: write-through */);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains ...
-            __syncthreads();                                   // ... before the ticket
-            if (tid == 0) {
-                const unsigned old = __hip_atomic_fetch_add(ep.tile_cnt + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int last = old == (unsigned)(S - 1);
-                if (last) __hip_atomic_store(ep.tile_cnt + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_last = last;
-            }
-            __syncthreads();
-            if (!s_last) return;
-        }
-        for (int c = tid; c < BM * CPR; c += NT) {
-            const int lr = c / CPR, ch = c - lr * CPR;
-            const int row = m0 + lr;
-            if (row >= M) continue;
-            const int col = n0 + ch * 4;
-            float4* sp = reinterpret_cast<float4*>(smem + lr * SROW + ch * 16);
-            float4 v = *sp;
-            if (S > 1) {
-                float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
-                for (int sl = 0; sl < S; ++sl) {
-                    float4 p = v;
-                    if (sl != split) {
-                        const long long off = ((long long)sl * ep.split_stride + (long long)row * ep.ldws + col) * 4;
-                        const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(wsr, (int)off, 0, 16 /* sc1 */);
-                        p = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
-                    }
-                    sum.x += p.x;
-                    sum.y += p.y;
-                    sum.z += p.z;
-                    sum.w += p.w;
-                }
-                v = sum;
-            }
-            const float4 b = ep.bias ? *reinterpret_cast<const float4*>(ep.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 x = *reinterpret_cast<const float4*>(ep.resid + (size_t)row * ep.ldr + col);
-            v.x = (v.x + b.x) + x.x;
-            v.y = (v.y + b.y) + x.y;
-            v.z = (v.z + b.z) + x.z;
-            v.w = (v.w + b.w) + x.w;
-            *sp = v;
-            *reinterpret_cast<float4*>(reinterpret_cast<float*>(ep.out) + (size_t)row * ep.ldo + col) = v;
-            *reinterpret_cast<uint2*>(ep.out2 + (size_t)row * ep.ldo2 + col) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
-        }
-        __syncthreads();
-        constexpr int SPR = BN / LN_SLICE;
-        for (int t = tid; t < BM * SPR; t += NT) {
-            const int lr = t / SPR, sl = t - lr * SPR;
-            const int row = m0 + lr;
-            if (row >= M) continue;
-            const float4* p = reinterpret_cast<const float4*>(smem + lr * SROW + sl * LN_SLICE * 4);
-            float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-            for (int e = 0; e < LN_SLICE / 4; ++e) {
-                const float4 f = p[e];
-                s1 += (f.x + f.y) + (f.z + f.w);
-                s2 = fmaf(f.x, f.x, fmaf(f.y, f.y, fmaf(f.z, f.z, fmaf(f.w, f.w, s2))));
-            }
-            reinterpret_cast<float2*>(ep.ln_stats)[(size_t)row * ep.ln_nst + n0 / LN_SLICE + sl] = make_float2(s1, s2);
-        }
-        return;
-    }
-
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_PARTIAL ||
                   EPI == EPI_QKV) {
         // LDS-staged store: the MFMA layout puts 16 consecutive columns on 16 lanes (2-4 B each), so
@@ -501,23 +353,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
         __syncthreads();                   // every wave is done reading the last ring stage
         const int lrow0 = wm * WTM + (lane >> 4) * 4;
         const int lcol0 = wn * WTN + (lane & 15);
-        float2 st[TM][4];
-        if constexpr (LNF) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) st[i][r] = ln_stat[lrow0 + i * 16 + r];
-        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const float bv = (EPI != EPI_PARTIAL && ep.bias) ? ep.bias[n0 + lcol0 + j * 16] : 0.f;
-            const float c1 = LNF ? ep.ln_c1[n0 + lcol0 + j * 16] : 0.f;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     float v = acc[i][j][r] + bv;
-                    if constexpr (LNF) v = st[i][r].y * fmaf(-st[i][r].x, c1, acc[i][j][r]) + bv;
                     if constexpr (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
                     if constexpr (EPI == EPI_GELU_ERF) v = gelu_erf(v);
                     char* dst = smem + (lrow0 + i * 16 + r) * SROW + (lcol0 + j * 16) * OB;
@@ -608,9 +451,9 @@ static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw
                                   const GemmEpi& ep, hipStream_t stream) {
     g_tile_count[BM <= 32 ? 0 : BM <= 64 ? 1 : BM <= 128 ? 2 : 3][BN <= 64 ? 0 : BN <= 96 ? 1 : BN <= 128 ? 2 : 3]
         .fetch_add(1, std::memory_order_relaxed);
-    const int tiles = ((M + BM - 1) / BM) * (N / BN) * ((EPI == EPI_PARTIAL || EPI == EPI_RESID_LN) ? ep.split_k : 1);
+    const int tiles = ((M + BM - 1) / BM) * (N / BN) * (EPI == EPI_PARTIAL ? ep.split_k : 1);
     size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
-    const size_t stage_out = (size_t)BM * (BN * (EPI == EPI_PARTIAL || EPI == EPI_RESID_LN ? 4 : 2) + 16);  // LDS-staged epilogue
+    const size_t stage_out = (size_t)BM * (BN * (EPI == EPI_PARTIAL ? 4 : 2) + 16);  // LDS-staged epilogue
     if (EPI != EPI_ARGMAX && EPI != EPI_F32 && stage_out > lds) lds = stage_out;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
@@ -640,18 +483,6 @@ static bool gemm96_on() {
     }
     return v == 1;
 }  // tuning override (dlms_gemm_force_tile), -1 = heuristic
-// big-M GEMMs (prefill): unset -> 128x128 tiles with MODE 3; DLMS_GEMM_BIG_MODE=0..3 -> the
-// 256x256 tile with that MODE (0 plain, 1 REGPF, 2 GROUPED, 3 both), the A/B of
-// profiles/r4_prefill_gemm_modes.jsonl
-static int big_mode() {
-    static int v = -2;
-    if (v == -2) {
-        const char* e = getenv("DLMS_GEMM_BIG_MODE");
-        v = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
-    }
-    return v;
-}
-
 template <int EPI, int IN>
 static hipError_t launch_forced(int id, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                 const GemmEpi& ep, hipStream_t stream, bool* done) {
@@ -699,28 +530,13 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
     // (not for the fp32 split-K epilogue: its 256 x 1 KiB staged rows exceed the LDS)
     if (N % 256 == 0 && id == 14 && EPI != EPI_PARTIAL)
         return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
-    // big-GEMM modes (REGPF = 1, GROUPED = 2, both = 3)
-    if constexpr (IN == IN_BF16 && EPI != EPI_RESID_LN) {
-        if (N % 256 == 0 && EPI != EPI_PARTIAL) {
-            switch (id) {
-                case 20: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
-                case 21: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
-                case 22: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
-                default: break;
-            }
-        }
-        // all rows of a decode half in one row tile (the LM head: W streamed once, A re-read from
-        // L2) -- measured slower than gemm_ps at 512 rows: 89.3 / 73.3 (256x64) vs 67.9 us
-        // (profiles/r4_lmhead_tiles_m512.jsonl), kept as forced configs for the bench
-        switch (id) {
-            case 26: return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 0>(A, lda, W, ldw, M, N, K, ep, stream);
-            case 27: return launch_gemm_cfg<512, 64, 8, 1, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
-            case 28: return launch_gemm_cfg<256, 64, 4, 1, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
-            default: break;
-        }
+    // the big-GEMM modes on 128x128 tiles (the prefill default; REGPF = 1, GROUPED = 2, both = 3) for
+    // the forced-tile tests: 24 = both, 25 = GROUPED.  (Round 4's 256x256 / 256x128 mode variants and
+    // the one-row-tile LM heads, all measured slower, were removed: profiles/r4_prefill_gemm_modes.jsonl,
+    // r4_lmhead_tiles_m512.jsonl.)
+    if constexpr (IN == IN_BF16) {
         if (N % 128 == 0) {
             switch (id) {
-                case 23: return launch_gemm_cfg<256, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
                 case 24: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
                 case 25: return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
                 default: break;
@@ -731,31 +547,9 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
     return hipSuccess;
 }
 
-// The LayerNorm-folded decode chain of the 512-row halves (EPI_RESID_LN producers, MODE_LNF
-// consumers): the tiles of the plain split-K / 64x96 rules below, nothing else instantiated
-static hipError_t launch_resid_ln(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
-                                  const GemmEpi& ep, hipStream_t stream) {
-    // c_proj on a decode half (K 3072, split 4): 64x96 tiles, 256 workgroups; the out-projection
-    // (K 768, split 2): 64x64 tiles, 192 workgroups
-    if (N % 96 == 0 && ep.split_k == 4 && M > 256 && M <= 512 && K >= 2048)
-        return launch_gemm_cfg<64, 96, 2, 2, 4, EPI_RESID_LN, IN_BF16>(A, lda, W, ldw, M, N, K, ep, stream);
-    return launch_gemm_cfg<64, 64, 2, 2, 4, EPI_RESID_LN, IN_BF16>(A, lda, W, ldw, M, N, K, ep, stream);
-}
-
-template <int EPI>
-static hipError_t launch_lnf(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const GemmEpi& ep,
-                             hipStream_t stream) {
-    if (N % 96 == 0 && M > 256 && M <= 512 && N != 768 && (long)((M + 63) / 64) * (N / 96) <= 256)
-        return launch_gemm_cfg<64, 96, 2, 2, 4, EPI, IN_BF16, MODE_LNF>(A, lda, W, ldw, M, N, K, ep, stream);
-    return launch_gemm_cfg<64, 64, 2, 2, 4, EPI, IN_BF16, MODE_LNF>(A, lda, W, ldw, M, N, K, ep, stream);
-}
-
 template <int EPI, int IN>
 static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
-    if constexpr (IN == IN_BF16 && (EPI == EPI_QKV || EPI == EPI_GELU_TANH || EPI == EPI_BF16)) {
-        if (ep.ln_fold) return launch_lnf<EPI>(A, lda, W, ldw, M, N, K, ep, stream);
-    }
     const int split = EPI == EPI_PARTIAL ? ep.split_k : 1;
     if (g_force_tile >= 0) {
         bool done = false;
@@ -775,7 +569,7 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
                                     EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
         // (only at the measured size class: 1024-prompt packed prefills; smaller admissions keep the
         // tiles below, e.g. a 4096-row out-projection would put 192 128x128 tiles on 256 CUs)
-        if (big_mode() < 0 && M >= 16384 && N % 128 == 0)
+        if (M >= 16384 && N % 128 == 0)
             return launch_gemm_cfg<128, 128, 2, 2, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
     }
     // big prefill GEMMs with a bf16 epilogue: 256x256 tiles, 8 waves of 128x64 (one workgroup per
@@ -785,15 +579,6 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF || EPI == EPI_QKV) {
         const long t256 = (long)((M + 255) / 256) * (N / 256);
         if (N % 256 == 0 && M >= 4096 && (t256 <= 256 || t256 % 256 >= 128 || t256 >= 512)) {
-            if constexpr (IN == IN_BF16) {
-                switch (big_mode()) {
-                    case 0: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
-                    case 1: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 1>(A, lda, W, ldw, M, N, K, ep, stream);
-                    case 2: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 2>(A, lda, W, ldw, M, N, K, ep, stream);
-                    case 3: return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN, 3>(A, lda, W, ldw, M, N, K, ep, stream);
-                    default: break;
-                }
-            }
             return launch_gemm_cfg<256, 256, 2, 4, 2, EPI, IN>(A, lda, W, ldw, M, N, K, ep, stream);
         }
     }
@@ -851,15 +636,7 @@ extern "C" long dlms_gemm_tile_count(int bm, int bn) {
 extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                 const GemmEpi* ep, hipStream_t stream) {
     if (K % GEMM_BK != 0 || N % 64 != 0 || M <= 0) return hipErrorInvalidValue;
-    if ((epi == EPI_PARTIAL || epi == EPI_RESID_LN) && (ep->split_k < 1 || K % (ep->split_k * GEMM_BK) != 0))
-        return hipErrorInvalidValue;
-    if (epi == EPI_RESID_LN && (!ep->out || !ep->out2 || !ep->resid || !ep->ln_stats || N % LN_SLICE != 0 ||
-                                ep->ln_nst * LN_SLICE < N || (ep->split_k > 1 && (!ep->ws || !ep->tile_cnt)) ||
-                                (long long)ep->split_k * ep->split_stride * 4 > 0x7fffffffLL))
-        return hipErrorInvalidValue;
-    if (ep->ln_fold && (epi == EPI_QKV || epi == EPI_GELU_TANH || epi == EPI_BF16) &&
-        (!ep->ln_stats || !ep->ln_c1 || ep->ln_nst < 1 || ep->ln_nst > LNF_MAX_SLOTS || ep->ln_k < 1))
-        return hipErrorInvalidValue;
+    if (epi == EPI_PARTIAL && (ep->split_k < 1 || K % (ep->split_k * GEMM_BK) != 0)) return hipErrorInvalidValue;
     switch (epi) {
         case EPI_BF16: return launch_gemm_epi<EPI_BF16, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
         case EPI_GELU_TANH: return launch_gemm_epi<EPI_GELU_TANH, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
@@ -868,7 +645,6 @@ extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, 
         case EPI_QKV: return launch_gemm_epi<EPI_QKV, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
         case EPI_ARGMAX: return launch_gemm_epi<EPI_ARGMAX, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
         case EPI_PARTIAL: return launch_gemm_epi<EPI_PARTIAL, IN_BF16>(A, lda, W, ldw, M, N, K, *ep, stream);
-        case EPI_RESID_LN: return launch_resid_ln(A, lda, W, ldw, M, N, K, *ep, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -878,8 +654,7 @@ extern "C" hipError_t dlms_gemm(int epi, const void* A, int lda, const void* W, 
 // producer emits the row-scaled fp8 activation directly.
 extern "C" hipError_t dlms_gemm_fp8(int epi, const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                     const GemmEpi* ep, hipStream_t stream) {
-    if (K % (2 * GEMM_BK) != 0 || N % 64 != 0 || M <= 0 || !ep->a_scale || !ep->w_scale || ep->ln_fold)
-        return hipErrorInvalidValue;
+    if (K % (2 * GEMM_BK) != 0 || N % 64 != 0 || M <= 0 || !ep->a_scale || !ep->w_scale) return hipErrorInvalidValue;
     if (epi == EPI_PARTIAL && (ep->split_k < 1 || K % (ep->split_k * 2 * GEMM_BK) != 0)) return hipErrorInvalidValue;
     switch (epi) {
         case EPI_BF16: return launch_gemm_epi<EPI_BF16, IN_FP8>(A, lda, W, ldw, M, N, K, *ep, stream);

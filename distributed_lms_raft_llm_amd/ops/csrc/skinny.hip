@@ -31,17 +31,8 @@ enum { SK_BF16 = 0, SK_GELU_TANH = 1, SK_F32 = 3, SK_QKV = 4, SK_ARGMAX = 5, SK_
 
 // Weight-fragment loads: plain (default-policy) loads keep the streamed weights eligible for the
 // 256 MiB Infinity Cache, which holds most of GPT-2-small's 248 MB per-step weight stream at batch
-// 1; DLMS_SKINNY_NT=1 builds non-temporal loads instead (cdna guide: nt-weights row).
-#ifndef DLMS_SKINNY_NT
-#define DLMS_SKINNY_NT 0
-#endif
-__device__ __forceinline__ bf16x8_t load_wfrag(const bf16x8_t* p) {
-#if DLMS_SKINNY_NT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
+// 1 (non-temporal loads measured no better here: cdna guide nt-weights row).
+__device__ __forceinline__ bf16x8_t load_wfrag(const bf16x8_t* p) { return *p; }
 
 // The batch-1 LM head streams 77 MB once per token: non-temporal loads keep it from evicting the
 // 12 layers' ~170 MB of weights out of the 256 MiB Infinity Cache (a cyclic 248 MB stream through
@@ -960,7 +951,8 @@ extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long 
                                       const void* Wp_sl, const float* b_p, void* r_out, int ldr, long long rcs, int M,
                                       int K, int F, int want_cg, int base, hipStream_t stream) {
     if (M <= 0 || M > 8 || F % 16 || F <= 0) return hipErrorInvalidValue;
-    if (nsplit != 0 && nsplit != 1 && (nsplit != 4 || K > 1024)) return hipErrorInvalidValue;
+    if (nsplit != 0 && nsplit != 1 && !(nsplit == 4 && K <= 1280) && !(nsplit == 5 && K == 1600))
+        return hipErrorInvalidValue;
     const int cg = dlms_skinny_mlp_cg(K, M, want_cg);
     if (cg == 0) return hipErrorInvalidValue;
     const bf16_t* Wf = reinterpret_cast<const bf16_t*>(Wfc_sh);
@@ -980,10 +972,12 @@ extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long 
             if (nsplit == 4) MLP_K(4, 4, 32);
             if (nsplit == 1) MLP_K(1, 4, 32);
             MLP_K(0, 4, 32);
-        case 1280:
+        case 1280:  // (4 slabs: GPT-2-large's 20 heads in head groups of 5)
+            if (nsplit == 4) MLP_K(4, 5, 40);
             if (nsplit == 1) MLP_K(1, 5, 40);
             MLP_K(0, 5, 40);
-        case 1600:
+        case 1600:  // (5 slabs: GPT-2-XL's 25 heads in head groups of 5)
+            if (nsplit == 5) MLP_K(5, 7, 50);
             if (nsplit == 1) MLP_K(1, 7, 50);
             MLP_K(0, 7, 50);
         default: return hipErrorInvalidValue;
@@ -1081,10 +1075,8 @@ __global__ __launch_bounds__(64 * NW) void attn_split_kernel(const bf16_t* __res
 
     float m = -INFINITY, l = 0.f;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#ifndef DLMS_SPLIT_U
-#define DLMS_SPLIT_U 4
-#endif
-    constexpr int U = DLMS_SPLIT_U;  // key groups of 8 in flight per wave
+
+    constexpr int U = 4;  // key groups of 8 in flight per wave (profiles/r2_attn_split_unroll.txt)
     for (int t0 = t_lo; t0 < t_hi; t0 += 8 * U) {
         uint4 kr[U], vr[U];
 #pragma unroll
@@ -1405,17 +1397,20 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(
     }
 }
 
-// Head-grouped variant for ONE row (batch 1): workgroup (g, j) covers HG heads with 4 waves per
-// head (keys split 4 ways, log-sum-exp merge in LDS) and their 2*HG k-blocks of its NT W_o tiles,
+// Head-grouped variant for ONE row (batch 1): workgroup (g, j) covers HG heads with WPH waves per
+// head (keys split WPH ways, log-sum-exp merge in LDS) and their 2*HG k-blocks of its NT W_o tiles,
 // so the out-projection lands in H / HG slabs instead of H -- with HG = H / 4 exactly the four
 // split-K slabs the fused add+LN kernel already sums (12 slabs cost that kernel ~2 us at batch 1).
-template <int HG, int NT>
-__global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
+// GPT-2-large / XL (20 / 25 heads): groups of 5 heads, 2 waves per head (a workgroup holds at most
+// 16 waves) -> 4 / 5 slabs for the fused MLP.
+template <int HG, int NT, int WPH>
+__global__ __launch_bounds__(64 * WPH * HG) void attn_oproj_hg_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int* __restrict__ row_slot, const int* __restrict__ row_kvlen, int H, int t_max, int n_slots,
     float scale_log2, const bf16_t* __restrict__ Wo_sh, int N, float* __restrict__ part, long long split_stride) {
-    constexpr int NW = 4 * HG;
-    constexpr int U = HG >= 4 ? 4 : 8;  // 16 waves per CU leave 128 VGPRs per lane
+    constexpr int NW = WPH * HG;
+    static_assert(NW <= 16 && NT <= NW && 16 * 8 * HG <= 64 * NW, "workgroup geometry");
+    constexpr int U = NW >= 16 ? 4 : 8;  // 16 waves per CU leave 128 VGPRs per lane
     constexpr int AW = HG * 64 + 8;  // A image row (bf16), padded
     __shared__ float part_s[NW][8][10];
     __shared__ __attribute__((aligned(16))) bf16_t aimg[16][AW];
@@ -1435,14 +1430,14 @@ __global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
         for (int k = 0; k < 2 * HG; ++k) wb[k] = src[k * 64];
     }
 
-    // (1) attention: wave w -> head grp*HG + w/4, key slice w%4
-    const int hh = wave >> 2, sl = wave & 3;
+    // (1) attention: wave w -> head grp*HG + w/WPH, key slice w%WPH
+    const int hh = wave / WPH, sl = wave % WPH;
     const int h = grp * HG + hh;
     const int g = lane >> 3, c = lane & 7;
     const int slot = (int)dlms_idx(row_slot[0], n_slots, CHK_ATTN_SLOT);
     int kvlen = row_kvlen[0];
     kvlen = kvlen < 1 ? 1 : (kvlen > t_max ? t_max : kvlen);
-    const int span = ((kvlen + 3) / 4 + 7) & ~7;
+    const int span = ((kvlen + WPH - 1) / WPH + 7) & ~7;
     const int t_lo = sl * span < kvlen ? sl * span : kvlen;
     const int t_hi = t_lo + span < kvlen ? t_lo + span : kvlen;
     const size_t head_off = ((size_t)slot * H + h) * t_max * 64;
@@ -1515,16 +1510,16 @@ __global__ __launch_bounds__(256 * HG) void attn_oproj_hg_kernel(
         if (r == 0) {
             float M_ = -INFINITY;
 #pragma unroll
-            for (int w = 0; w < 4; ++w) M_ = fmaxf(M_, part_s[hh2 * 4 + w][cc][0]);
+            for (int w = 0; w < WPH; ++w) M_ = fmaxf(M_, part_s[hh2 * WPH + w][cc][0]);
             float L = 0.f;
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const float mw = part_s[hh2 * 4 + w][cc][0];
+            for (int w = 0; w < WPH; ++w) {
+                const float mw = part_s[hh2 * WPH + w][cc][0];
                 if (mw == -INFINITY) continue;
                 const float f = exp2f(mw - M_);
-                L += part_s[hh2 * 4 + w][cc][1] * f;
+                L += part_s[hh2 * WPH + w][cc][1] * f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) o8[e] += part_s[hh2 * 4 + w][cc][2 + e] * f;
+                for (int e = 0; e < 8; ++e) o8[e] += part_s[hh2 * WPH + w][cc][2 + e] * f;
             }
             const float inv = 1.f / L;
 #pragma unroll
@@ -1549,7 +1544,7 @@ extern "C" hipError_t dlms_attention_oproj_grouped(const void* q, const void* kc
                                                    const int* row_kvlen, int H, int hg, int t_max, int n_slots,
                                                    float scale, const void* wo_sh, int N, int nt, float* part,
                                                    long long split_stride, hipStream_t stream) {
-    if (H < 1 || hg < 1 || H % hg || t_max < 1 || N % 16 || nt < 1 || nt > 4 * hg || (N / 16) % nt)
+    if (H < 1 || hg < 1 || H % hg || t_max < 1 || N % 16 || nt < 1 || nt > (hg == 5 ? 10 : 4 * hg) || (N / 16) % nt)
         return hipErrorInvalidValue;
     const float sl2 = scale * 1.4426950408889634f;
     const dim3 grid(H / hg, (N / 16) / nt);
@@ -1559,9 +1554,10 @@ extern "C" hipError_t dlms_attention_oproj_grouped(const void* q, const void* kc
                            row_kvlen, H, t_max, n_slots, sl2, reinterpret_cast<const bf16_t*>(wo_sh), N, part,
                            split_stride);
     };
-#define AOG(HG_, NT_) \
-    if (hg == HG_ && nt == NT_) { go(attn_oproj_hg_kernel<HG_, NT_>, 256 * HG_); return hipGetLastError(); }
-    AOG(3, 1) AOG(3, 2) AOG(3, 3) AOG(3, 4) AOG(4, 1) AOG(4, 2) AOG(4, 3) AOG(4, 4)
+#define AOG(HG_, NT_, WPH_) \
+    if (hg == HG_ && nt == NT_) { go(attn_oproj_hg_kernel<HG_, NT_, WPH_>, 64 * WPH_ * HG_); return hipGetLastError(); }
+    AOG(3, 1, 4) AOG(3, 2, 4) AOG(3, 3, 4) AOG(3, 4, 4) AOG(4, 1, 4) AOG(4, 2, 4) AOG(4, 3, 4) AOG(4, 4, 4)
+    AOG(5, 4, 2) AOG(5, 5, 2) AOG(5, 10, 2)
 #undef AOG
     return hipErrorInvalidValue;
 }

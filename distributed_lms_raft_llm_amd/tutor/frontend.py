@@ -245,7 +245,11 @@ class FrontendPool:
         try:
             item = (rid, fut.result(), "OK", "")
         except BaseException as e:  # batcher failure: UNAVAILABLE so clients fail over
+            from ..engine.scheduler import Overloaded
+
             code = "UNAVAILABLE" if getattr(self.batcher, "failed", None) is not None else "INTERNAL"
+            if isinstance(e, Overloaded):
+                code = "RESOURCE_EXHAUSTED"
             item = (rid, None, code, str(e))
         with self._cv:
             self._out[i].append(item)

@@ -28,6 +28,7 @@ import grpc
 import torch
 
 from .. import wire
+from ..engine.scheduler import Overloaded
 from ..models.config import GenerationConfig, gpt2_config
 from ..models.gpt2 import init_gpt2_weights, load_safetensors_weights
 from ..tokenizer import GPT2BPE
@@ -40,6 +41,13 @@ log = logging.getLogger("dlms.tutor")
 
 PROMPT_TEMPLATE = ("You are an intelligent assistant. Answer the following question in detail:\n"
                    "Question: {query}\nAnswer:")
+
+
+def default_max_queue(engine, max_queue: int | None) -> int:
+    """Admission limit of a serving replica: queries that may wait for a KV slot beyond the
+    engine's slots (one batch of slots by default -- about one generation of queueing delay)
+    before it answers RESOURCE_EXHAUSTED; 0 = unbounded."""
+    return engine.max_batch if max_queue is None else int(max_queue)
 
 
 def build_prompt(query: str) -> str:
@@ -127,6 +135,8 @@ class TutoringServicer:
         ids = self.tok.encode(build_prompt(request.query))
         try:
             out = self.batcher.submit(ids).result(timeout=self.timeout)
+        except Overloaded as e:  # shed load now rather than queue past the client's deadline
+            context.abort(grpc.StatusCode.RESOURCE_EXHAUSTED, str(e))
         except Exception as e:
             # a failed batcher (e.g. a tensor-parallel peer stalled in an xGMI collective) will not
             # serve again in this process: UNAVAILABLE makes the LMS's TutoringClient fail over to
@@ -163,7 +173,7 @@ def make_engine(model: str, device: str, max_batch: int, max_length: int, weight
 class TutoringServer:
     def __init__(self, engine, port: int = 50054, host: str = "[::]", max_batch: int = 64, window_ms: float = 2.0,
                  max_length: int = 150, repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None,
-                 workers: int = 64, batching: str = "auto", chunk: int = 8):
+                 workers: int = 64, batching: str = "auto", chunk: int = 8, max_queue: int | None = None):
         self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
         self.tok = tokenizer or GPT2BPE(eos_token_id=getattr(getattr(engine, "cfg", None), "eos_token_id", 50256))
         if batching == "auto":
@@ -173,7 +183,8 @@ class TutoringServer:
 
             if engine.max_length != max_length:
                 raise ValueError("continuous batching: engine max_length differs from the server's")
-            self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
+            self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk,
+                                             max_queue=default_max_queue(engine, max_queue))
         else:
             self.batcher = Batcher(engine, self.gen, max_batch=max_batch, window_ms=window_ms)
         self.batching = batching
@@ -249,6 +260,8 @@ class AioTutoringServicer:
         ids = self.tok.encode(build_prompt(request.query))
         try:
             out = await asyncio.wait_for(asyncio.wrap_future(self.batcher.submit(ids)), self.timeout)
+        except Overloaded as e:
+            await context.abort(grpc.StatusCode.RESOURCE_EXHAUSTED, str(e))
         except Exception as e:
             failed = getattr(self.batcher, "failed", None) is not None
             code = grpc.StatusCode.UNAVAILABLE if failed else grpc.StatusCode.INTERNAL
@@ -263,7 +276,8 @@ class AioTutoringServer(TutoringServer):
     fatal hook and stop() as ``TutoringServer``."""
 
     def __init__(self, engine, port: int = 50054, host: str = "[::]", max_length: int = 150,
-                 repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None, chunk: int = 8):
+                 repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None, chunk: int = 8,
+                 max_queue: int | None = None):
         import asyncio
 
         from ..engine.scheduler import ContinuousBatcher
@@ -274,7 +288,8 @@ class AioTutoringServer(TutoringServer):
             raise ValueError("continuous batching: engine max_length differs from the server's")
         self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
         self.tok = tokenizer or GPT2BPE(eos_token_id=getattr(getattr(engine, "cfg", None), "eos_token_id", 50256))
-        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
+        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk,
+                                             max_queue=default_max_queue(engine, max_queue))
         self.batching = "continuous"
         self.engine = engine
         self._stopping = threading.Event()
@@ -320,7 +335,8 @@ class PooledTutoringServer(TutoringServer):
     the front ends, which share the public port.  Same health/metrics surface, fatal hook and
     stop() as ``TutoringServer``."""
 
-    def __init__(self, engine, pool, max_length: int = 150, repetition_penalty: float = 1.2, chunk: int = 8):
+    def __init__(self, engine, pool, max_length: int = 150, repetition_penalty: float = 1.2, chunk: int = 8,
+                 max_queue: int | None = None):
         from ..engine.scheduler import ContinuousBatcher
 
         if not hasattr(engine, "admit"):
@@ -328,7 +344,8 @@ class PooledTutoringServer(TutoringServer):
         if engine.max_length != max_length:
             raise ValueError("continuous batching: engine max_length differs from the server's")
         self.gen = GenerationConfig(max_length=max_length, repetition_penalty=repetition_penalty)
-        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk)
+        self.batcher = ContinuousBatcher(engine, repetition_penalty, chunk=chunk,
+                                             max_queue=default_max_queue(engine, max_queue))
         self.batching = "continuous"
         self.engine = engine
         self.pool = pool
@@ -373,6 +390,9 @@ def main(argv=None):
     ap.add_argument("--tp", type=int, default=0, help="tensor-parallel degree under torchrun (default: world)")
     ap.add_argument("--batching", choices=("auto", "continuous", "window"), default="auto")
     ap.add_argument("--chunk", type=int, default=8, help="decode steps between scheduler polls")
+    ap.add_argument("--max-queue", type=int, default=None,
+                    help="queries that may wait for a KV slot before the replica answers RESOURCE_EXHAUSTED "
+                         "(default: one batch of slots; 0 = unbounded)")
     ap.add_argument("--frontend", choices=("aio", "threads"), default="aio",
                     help="aio: asyncio gRPC front end (thousands of queries in flight); threads: a worker per query")
     ap.add_argument("--frontends", type=int, default=4,
@@ -425,7 +445,8 @@ def main(argv=None):
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     if pool is not None and hasattr(eng, "admit"):
-        srv = PooledTutoringServer(eng, pool, args.max_length, args.repetition_penalty, chunk=args.chunk)
+        srv = PooledTutoringServer(eng, pool, args.max_length, args.repetition_penalty, chunk=args.chunk,
+                                   max_queue=args.max_queue)
     else:
         if pool is not None:  # not a slot engine (CPU window batching): serve in-process
             pool.stop(timeout=2)
@@ -434,10 +455,11 @@ def main(argv=None):
         pass
     elif args.frontend == "aio" and args.batching != "window" and hasattr(eng, "admit"):
         srv = AioTutoringServer(eng, args.port, args.host, args.max_length, args.repetition_penalty, tokenizer=tok,
-                                chunk=args.chunk)
+                                chunk=args.chunk, max_queue=args.max_queue)
     else:
         srv = TutoringServer(eng, args.port, args.host, args.max_batch, args.window_ms, args.max_length,
-                             args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk)
+                             args.repetition_penalty, tokenizer=tok, batching=args.batching, chunk=args.chunk,
+                             max_queue=args.max_queue)
     done = threading.Event()
     fatal: list = []
 

@@ -15,6 +15,11 @@ seconds (discarded: hipGraph capture of new batch buckets, channel setup) follow
                          are waited for), ``inflight_mean``/``inflight_max`` summed over clients;
 * ``server``          -- the server's queue / ttft / request-latency histograms.
 
+``--closed N`` (one client process): N closed-loop clients instead of the Poisson stream, each
+sending its next query the moment the previous answer arrives -- ``--closed 1`` is the reference's
+own operating point, one student query at a time (``lms_server.py:1237-1274``); the line then also
+reports the dataflow-kernel aborts the tutor counted in the window.
+
 ``--engine null`` replaces the GPT-2 engine by a host-only slot engine (fixed ``--null-step-ms``
 per decode step): it measures the gRPC front end's own ceiling on any machine.
 
@@ -93,6 +98,18 @@ def _client_main(conn):
         while time.time() < t_begin:
             await asyncio.sleep(min(0.05, t_begin - time.time()))
         samp = asyncio.ensure_future(sampler())
+        if cfg.get("closed"):
+            async def loop(j):
+                k = j
+                while time.time() < t_stop:
+                    await one(k, time.time())
+                    k += cfg["closed"]
+
+            await asyncio.gather(*(loop(j) for j in range(cfg["closed"])))
+            await samp
+            for c in chans:
+                await c.close()
+            return recs, samples
         tasks = set()
         t_next, k = t_begin, 0
         while True:
@@ -323,11 +340,15 @@ def main():
     ap.add_argument("--students", type=int, default=64)
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--startup-timeout", type=float, default=600.0)
+    ap.add_argument("--closed", type=int, default=0,
+                    help="N closed-loop clients (one query at a time each) instead of open-loop --rates")
     ap.add_argument("--out", default=None, help="append JSON lines here")
     ap.add_argument("--log", default=None, help="server stdout/stderr")
     ap.add_argument("--tag", default="")
     ap.add_argument("--serve-null", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.closed:
+        args.client_procs, args.rates = 1, "0"
     if args.serve_null:
         return serve_null(args.frontends, args.null_slots, args.max_length, args.null_step_ms, args.chunk)
 
@@ -365,7 +386,7 @@ def main():
             for i, (_, conn) in enumerate(clients):
                 conn.send({"addrs": addrs, "service": service, "rate": rate / len(clients), "t_begin": t_begin,
                            "t_stop": t_stop, "calls": calls[i::len(clients)], "seed": 7919 * i + int(rate),
-                           "timeout": args.timeout, "channels": args.channels})
+                           "timeout": args.timeout, "channels": args.channels, "closed": args.closed})
             time.sleep(max(0.0, t_meas - time.time()))
             m0, w0 = metrics(tutor_addr), time.time()
             time.sleep(max(0.0, t_stop - time.time()))
@@ -395,7 +416,8 @@ def main():
             line = {
                 "bench": "serving_grpc", "target": f"{service}.GetLLMAnswer", "engine": args.engine,
                 "model": args.model, "tag": args.tag,
-                "offered_qps": rate, "duration_s": args.duration, "warmup_s": args.warmup,
+                "offered_qps": rate if not args.closed else None, "closed_clients": args.closed or None,
+                "duration_s": args.duration, "warmup_s": args.warmup,
                 "client_procs": args.client_procs, "nodes": 3 if args.target == "lms" else 0,
                 "gate": args.gate if args.target == "lms" else None,
                 "tok_s": round(tokens_win / (w1 - w0), 1),
@@ -412,6 +434,8 @@ def main():
                            for k in ("tutor_queue_ms", "tutor_ttft_ms", "tutor_request_ms", "tutor_tpot_ms")
                            if k in hist},
                 "boot_s": round(boot_s, 1),
+                "dataflow_aborts": c1.get("engine_dataflow_aborts", 0.0) - c0.get("engine_dataflow_aborts", 0.0),
+                "dataflow_aborts_total": c1.get("engine_dataflow_aborts", 0.0),
             }
             if lms_m:
                 line["lms_nodes"] = {

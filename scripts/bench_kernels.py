@@ -136,16 +136,10 @@ def main():
         o = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
         for Lk in (32, 90, args.T):
             kvl = torch.full((M,), Lk, dtype=torch.int32, device=dev)
-            for impl in ("wave0", "wave1", "wave2", "wave3", "lds"):
+            for impl in ("wave", "persist", "lds"):
                 if "attn" not in ops_on:
                     break
-                if impl.startswith("wave"):
-                    L.dlms_attention_variant(int(impl[4:]))
-                try:
-                    med, mn = graph_time(lambda i, impl=impl: ops.row_attention(
-                        q, kc, vc, slot, kvl, out=o, impl="lds" if impl == "lds" else "wave"))
-                finally:
-                    L.dlms_attention_variant(0)
+                med, mn = graph_time(lambda i, impl=impl: ops.row_attention(q, kc, vc, slot, kvl, out=o, impl=impl))
                 byts = M * H * Lk * 64 * 2 * 2
                 rec(M=M, op="attn", variant=f"{impl}_T{Lk}", us=round(med, 2), us_min=round(mn, 2),
                     GBps=round(byts / med / 1e3, 1))

@@ -6,7 +6,7 @@ idle gaps.  usage: timeline.py <kernel_trace.csv>
 Caveat (measured): under rocprofv3 --kernel-trace the overlapped step ran at 2150 us vs 1490 us
 unprofiled and the two queues barely overlapped (profiles/r2_timeline_b1024_profiled.txt), so the
 tracer itself serialises much of the concurrency; forcing the attentions to alternate between the
-queues (DLMS_OVERLAP_ALT_ATTN=1) was 4 % SLOWER unprofiled (profiles/r2_sweep_alt_attn.jsonl)."""
+queues (the since-removed alternating-attention schedule) was 4 % SLOWER unprofiled (profiles/r2_sweep_alt_attn.jsonl)."""
 import csv
 import sys
 from collections import defaultdict

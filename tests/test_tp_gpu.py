@@ -45,7 +45,7 @@ def _setup(geo="tp5"):
     return cfg, w, prompts
 
 
-def _worker(rank, world, port, q, p2p=False, geo="tp5"):
+def _worker(rank, world, port, q, p2p=False, geo="tp5", wdt="bf16"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -54,8 +54,9 @@ def _worker(rank, world, port, q, p2p=False, geo="tp5"):
 
         cfg, w, prompts = _setup(geo)
         # p2p: one-shot xGMI kernels instead of gloo calls -- all on the GPU, so hipGraph capture works
-        eng = HipGPT2Engine(cfg, w, max_batch=4, max_length=64, tp_group=dist.group.WORLD, use_graph=p2p, p2p=p2p)
-        assert (eng.xgmi is not None) == p2p
+        eng = HipGPT2Engine(cfg, w, max_batch=4, max_length=64, tp_group=dist.group.WORLD, use_graph=p2p, p2p=p2p,
+                            weight_dtype=wdt)
+        assert (eng.xgmi is not None) == p2p and eng.w.fp8 == (wdt == "fp8")
         hid = eng.prefill_last_hidden(prompts).cpu()
         out = eng.generate(prompts)
         fused = eng.tp_fused_steps
@@ -70,8 +71,11 @@ def _worker(rank, world, port, q, p2p=False, geo="tp5"):
         dist.destroy_process_group()
 
 
-def _run_tp(geo, world, p2p):
-    """TP=world ranks on cuda:0 vs TP=1, both margin-checked against the fp32 oracle."""
+def _run_tp(geo, world, p2p, wdt="bf16"):
+    """TP=world ranks on cuda:0 vs TP=1 bf16, both margin-checked against the fp32 oracle.  fp8 (W8A8
+    prefill, bf16 latency-path decode): last-token hidden states within cosine 0.99 of the bf16
+    TP=1 engine, and the oracle's token at every position whose top-1 / top-2 margin exceeds 0.5
+    (profiles/r5_config5_tp8_fp8_tests.txt)."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
     from distributed_lms_raft_llm_amd.engine.weights import shard_range
     from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, teacher_forced_check
@@ -85,7 +89,7 @@ def _run_tp(geo, world, p2p):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, p2p, geo)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, p2p, geo, wdt)) for r in range(world)]
     [p.start() for p in procs]
     try:
         res = sorted([q.get(timeout=800) for _ in range(world)], key=lambda r: r[0])
@@ -100,20 +104,24 @@ def _run_tp(geo, world, p2p):
     assert [r[4] for r in res] == [(a * 64, b * 64) for a, b in ftiles]
     for r in res:
         cos = torch.nn.functional.cosine_similarity(torch.from_numpy(r[2]), ref_hid, dim=-1)
-        assert bool((cos > 0.999).all()), cos
+        assert bool((cos > (0.99 if wdt == "fp8" else 0.999)).all()), cos
         assert r[3] == res[0][3]  # every rank emits the same tokens
     # margin-aware exactness against the fp32 oracle (teacher-forced on each engine's own output):
     # TP=world and TP=1 must both pick the oracle's greedy token wherever it is decisive
     oracle = GPT2Reference(cfg, w, device="cuda")
-    for outs in (res[0][3], ref_out):
+    # (fp8: the margin rule at 0.5 -- e4m3 rounding moves logits by more than the bf16 rule's 0.05 --,
+    # every such position the oracle's token; on this random-init geometry 25 of 139 positions
+    # clear 0.5, so at least 10 % are required to be decisive)
+    for outs, eps, frac in ((res[0][3], 0.5 if wdt == "fp8" else 0.05, 0.1 if wdt == "fp8" else 0.7),
+                            (ref_out, 0.05, 0.7)):
         decisive = total = 0
         for o, p in zip(outs, prompts):
             assert o[: len(p)] == p
-            r = teacher_forced_check(oracle, o, len(p), 1.2, eps=0.05)
+            r = teacher_forced_check(oracle, o, len(p), 1.2, eps=eps)
             assert not r["mismatches"], r["mismatches"]
             decisive += r["decisive"]
             total += r["positions"]
-        assert decisive >= 0.7 * total, (decisive, total)
+        assert decisive >= frac * total, (decisive, total)
     return res
 
 
@@ -133,3 +141,12 @@ def test_tp_configs_4_and_5_geometry_on_one_gpu(geo, world, p2p):
 def test_tp2_on_one_gpu_matches_tp1(p2p):
     res = _run_tp("tp5", 2, p2p)
     assert [r[1] for r in res] == [(0, 3), (3, 5)]
+
+
+@pytest.mark.parametrize("p2p", [False, True], ids=["gloo", "xgmi-graph"])
+def test_config5_xl_tp8_fp8_on_one_gpu(p2p):
+    """BASELINE config 5 as specified: GPT-2-XL geometry, TP=8, fp8 (W8A8 e4m3 QKV / c_fc / LM head in
+    the prefill and batches > 8; the bf16 six-kernel fused TP layer at these 3 rows), 8 ranks on one
+    GPU (VERDICT r4 next #3)."""
+    res = _run_tp("xl", 8, p2p, wdt="fp8")
+    assert [b - a for a, b in (r[1] for r in res)] == [4, 3, 3, 3, 3, 3, 3, 3]

@@ -55,14 +55,16 @@ class SlotEngine:
         return SimpleNamespace(result=lambda: word)
 
 
-def _server(engine, frontend="threads"):
+def _server(engine, frontend="threads", max_queue=None):
     fatal = threading.Event()
     if frontend == "aio":
-        srv = AioTutoringServer(engine, port=0, host="127.0.0.1", max_length=48, chunk=4)
+        srv = AioTutoringServer(engine, port=0, host="127.0.0.1", max_length=48, chunk=4, max_queue=max_queue)
     elif frontend == "pool":
-        srv = PooledTutoringServer(engine, FrontendPool(2, 0, "127.0.0.1"), max_length=48, chunk=4)
+        srv = PooledTutoringServer(engine, FrontendPool(2, 0, "127.0.0.1"), max_length=48, chunk=4,
+                                   max_queue=max_queue)
     else:
-        srv = TutoringServer(engine, port=0, host="127.0.0.1", max_length=48, batching="continuous", chunk=4)
+        srv = TutoringServer(engine, port=0, host="127.0.0.1", max_length=48, batching="continuous", chunk=4,
+                             max_queue=max_queue)
     srv.start(on_fatal=lambda e: fatal.set(), poll_s=0.02)
     return srv, fatal
 
@@ -122,7 +124,7 @@ def test_aio_frontend_serves_many_concurrent_requests(frontend):
     pool's front-end processes share the port)."""
     from concurrent import futures as cf
 
-    srv, fatal = _server(SlotEngine(max_batch=4), frontend)
+    srv, fatal = _server(SlotEngine(max_batch=4), frontend, max_queue=0)  # (no admission limit here)
     try:
         from distributed_lms_raft_llm_amd import wire
         from distributed_lms_raft_llm_amd.utils.debug_rpc import debug_call
@@ -141,3 +143,78 @@ def test_aio_frontend_serves_many_concurrent_requests(frontend):
         assert debug_call(f"127.0.0.1:{srv.port}", "Health")["ok"]
     finally:
         srv.stop()
+
+
+class SlowSlotEngine(SlotEngine):
+    def decode(self, B, steps, penalty):
+        import time
+
+        time.sleep(0.05)
+        super().decode(B, steps, penalty)
+
+
+@pytest.mark.parametrize("frontend", ["aio", "pool"])
+def test_overloaded_replica_refuses_fast_with_resource_exhausted(frontend):
+    """Admission control: with every KV slot busy and a full admission queue
+    (one batch of slots by default), a replica answers RESOURCE_EXHAUSTED at once instead of
+    queueing the query until its client deadline expires; the queries it admitted complete."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    from distributed_lms_raft_llm_amd import wire
+
+    srv, _ = _server(SlowSlotEngine(max_batch=2), frontend)
+    try:
+        s = wire.Stub("Tutoring", wire.channel(f"127.0.0.1:{srv.port}"))
+
+        def ask(k):
+            t0 = time.monotonic()
+            try:
+                r = s.GetLLMAnswer(pb.QueryRequest(token="t", query=f"q{k}"), timeout=60)
+                return "ok" if r.success else "fail", time.monotonic() - t0
+            except grpc.RpcError as e:
+                return e.code().name, time.monotonic() - t0
+
+        with ThreadPoolExecutor(16) as ex:
+            res = list(ex.map(ask, range(16)))
+        codes = [c for c, _ in res]
+        assert codes.count("ok") >= 2 and codes.count("RESOURCE_EXHAUSTED") >= 1, codes
+        assert set(codes) <= {"ok", "RESOURCE_EXHAUSTED"}, codes
+        # refused queries come back long before an admitted one finishes its 12 slow chunks
+        refused = [t for c, t in res if c == "RESOURCE_EXHAUSTED"]
+        served = [t for c, t in res if c == "ok"]
+        assert max(refused) < max(served), (refused, served)
+    finally:
+        srv.stop()
+
+
+def test_client_tries_another_replica_when_one_is_busy():
+    """RESOURCE_EXHAUSTED moves the query to the next replica without marking the busy one down;
+    when every replica refuses, the LMS answers "busy", not "unavailable"."""
+    from distributed_lms_raft_llm_amd.lms.service import MSG_TUTOR_BUSY, _tutor_error_message
+
+    class Busy(grpc.RpcError):
+        def code(self):
+            return grpc.StatusCode.RESOURCE_EXHAUSTED
+
+    calls = []
+
+    class Stub:
+        def __init__(self, i, busy):
+            self.i, self.busy = i, busy
+
+        def GetLLMAnswer(self, req, timeout=None):
+            calls.append(self.i)
+            if self.busy:
+                raise Busy()
+            return pb.QueryResponse(success=True, response="ok")
+
+    c = TutoringClient("a:1,b:2")
+    c._stubs = [Stub(0, True), Stub(1, False)]
+    assert c.ask("t", "q").response == "ok" and calls == [0, 1]
+    assert all(d == 0.0 for d in c._down_until)  # busy is not down
+    c._stubs = [Stub(0, True), Stub(1, True)]
+    with pytest.raises(grpc.RpcError) as ei:
+        c.ask("t", "q")
+    assert _tutor_error_message(ei.value) == MSG_TUTOR_BUSY
+    c.close()
