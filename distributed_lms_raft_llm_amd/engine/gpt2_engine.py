@@ -306,7 +306,7 @@ class HipGPT2Engine:
         # XL: groups of 5 heads -> 4 / 5 slabs, 5 W_o tiles per workgroup (64 / 100 workgroups)
         Hl = self.w.n_heads_local
         if self.fuse_ao and Hl in (20, 25):
-            self.ao_groups, self.ao_group_tiles = 5, 5
+            self.ao_groups, self.ao_group_tiles = 5, int(os.environ.get("DLMS_AO_TILES_EXP", "5"))
         else:
             self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4)) else 0
             self.ao_group_tiles = 3 if (cfg.n_embd // 16) % 3 == 0 else 1
