@@ -285,10 +285,11 @@ class HipGPT2Engine:
         # attention fused with the out-projection for <= 4 rows (one launch fewer per layer); its
         # workgroups recompute a head's attention, so only for short caches
         # (TP=1: its per-head slabs are summed by the next fused add+LN kernel, 12 or 16 of them)
-        # (GPT-2-large / XL's 20 / 25 heads: only the head-grouped batch-1 kernel, groups of 5)
+        # (GPT-2-large / XL's 20 / 25 heads in groups of 5 -- 2 waves per head, 4 / 5 slabs for the fused
+        # MLP -- measured slower than split attention + the in-place out-projection: large 131-135 vs
+        # 128 ms, XL 226-228 vs 211-212 ms per query, profiles/r5_large_xl_hg5_tiles_ab.jsonl; removed)
         self.fuse_ao = (self.small_max > 0 and self.tp_size == 1 and self.max_length <= 512 and
-                        (self.w.n_heads_local in (12, 16) and cfg.n_embd <= 1024 or
-                         self.w.n_heads_local in (20, 25) and cfg.n_embd in (1280, 1600)) and
+                        self.w.n_heads_local in (12, 16) and cfg.n_embd <= 1024 and
                         os.environ.get("DLMS_FUSE_ATTN_OPROJ", "1") != "0")
         if self.fuse_ao:
             try:
@@ -302,14 +303,10 @@ class HipGPT2Engine:
                     lw.w_o_sh = ops.shuffle_weight(lw.w_o)
             self.ao_parts = torch.zeros(self.w.n_heads_local, 4, cfg.n_embd, dtype=torch.float32, device=self.device)
         # batch 1: head groups of H/4 (3 or 4 heads) -> 4 slabs, 3 W_o tiles per workgroup
-        # (profiles/r2_attn_oproj_ab.txt: 36.6 vs 37.1 ms per query with one slab per head); GPT-2-large /
-        # XL: groups of 5 heads -> 4 / 5 slabs, 5 W_o tiles per workgroup (64 / 100 workgroups)
+        # (profiles/r2_attn_oproj_ab.txt: 36.6 vs 37.1 ms per query with one slab per head)
         Hl = self.w.n_heads_local
-        if self.fuse_ao and Hl in (20, 25):
-            self.ao_groups, self.ao_group_tiles = 5, int(os.environ.get("DLMS_AO_TILES_EXP", "5"))
-        else:
-            self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4)) else 0
-            self.ao_group_tiles = 3 if (cfg.n_embd // 16) % 3 == 0 else 1
+        self.ao_groups = Hl // 4 if (self.fuse_ao and Hl % 4 == 0 and Hl // 4 in (3, 4)) else 0
+        self.ao_group_tiles = 3 if (cfg.n_embd // 16) % 3 == 0 else 1
         self.ao_slabs = Hl // self.ao_groups if self.ao_groups else 0
         # batch 1 (TP=1, head-grouped attention): LN2 -> c_fc -> GELU -> c_proj as ONE kernel whose
         # workgroups add their 16-column slices into an int64 fixed-point residual (order-independent
@@ -847,8 +844,8 @@ class HipGPT2Engine:
     def _decode_layers_fused_mlp(self, r, B: int):
         """Layers as [LN1 + QKV (+ clear the MLP's accumulator)] -> attention + out-projection ->
         [add + LN2 + c_fc + GELU + c_proj, added into the int64 fixed-point residual xr[l % 2]].
-        Batch 1 with head groups (12 / 16 / 20 / 25 heads): attention fused with the out-projection (4 or
-        5 head-group slabs the MLP sums); otherwise split attention, then the skinny out-projection adding into the residual in place (the
+        Batch 1 with head groups (12 / 16 heads): attention fused with the out-projection (4 head-group
+        slabs the MLP sums); otherwise split attention, then the skinny out-projection adding into the residual in place (the
         f32 embedding rows x in layer 0, copy 0 of the fixed-point residual after that).  The final
         residual is xr[(L - 1) % 2]."""
         eps = self.cfg.layer_norm_epsilon

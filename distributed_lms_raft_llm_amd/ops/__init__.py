@@ -1015,9 +1015,8 @@ def skinny_mlp(x_in: torch.Tensor, gamma, beta, eps: float, w_fc_sh: torch.Tenso
         _req(t, torch.float32, n, 1)
         if t.numel() != size:
             raise ValueError(f"skinny_mlp: {n} size")
-    if nsplit not in (0, 1, 4, 5) or (nsplit == 4 and K > 1280) or (nsplit == 5 and K != 1600):
-        raise ValueError("skinny_mlp: nsplit in {0, 1, 4, 5} (4: d <= 1280 -- head groups of 3-5; 5: d 1600, "
-                         "GPT-2-XL's 25 heads in groups of 5)")
+    if nsplit not in (0, 1, 4) or (nsplit == 4 and K > 1024):
+        raise ValueError("skinny_mlp: nsplit in {0, 1, 4} (4: d <= 1024)")
     ldp, sstride = 0, 0
     if nsplit:
         _req(parts, torch.float32, "parts", 3)
@@ -1184,9 +1183,8 @@ def attention_oproj(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
 def attention_oproj_grouped(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, row_slot: torch.Tensor,
                             row_kvlen: torch.Tensor, wo_sh: torch.Tensor, parts: torch.Tensor, heads_per_group: int,
                             scale: float | None = None, tiles: int = 3) -> torch.Tensor:
-    """``attention_oproj`` for ONE row with heads in groups of ``heads_per_group`` (3, 4 or 5): group
-    g's share of the out-projection goes to ``parts[g, 0, :N]`` -- H / heads_per_group slabs.
-    (Groups of 5 -- GPT-2-large / XL -- run 2 waves per head; ``tiles`` then in {4, 5, 10}.)"""
+    """``attention_oproj`` for ONE row with heads in groups of ``heads_per_group`` (3 or 4): group g's
+    share of the out-projection goes to ``parts[g, 0, :N]`` -- H / heads_per_group slabs."""
     _req(q, torch.bfloat16, "q", 2)
     _req(k_cache, torch.bfloat16, "k_cache", 4)
     _req(v_cache, torch.bfloat16, "v_cache", 4)
@@ -1201,10 +1199,8 @@ def attention_oproj_grouped(q: torch.Tensor, k_cache: torch.Tensor, v_cache: tor
         raise ValueError("attention_oproj_grouped: one row")
     if hd != 64 or v_cache.shape != k_cache.shape or q.shape[1] < H * 64 or wo_sh.shape[1] * 32 != H * 64:
         raise ValueError("attention_oproj_grouped: bad shapes")
-    ok_tiles = (4, 5, 10) if hg == 5 else (1, 2, 3, 4)
-    if hg not in (3, 4, 5) or H % hg or (N // 16) % tiles or tiles not in ok_tiles:
-        raise ValueError("attention_oproj_grouped: heads_per_group in {3, 4, 5} dividing H, tiles dividing N/16 "
-                         f"and in {ok_tiles}")
+    if hg not in (3, 4) or H % hg or (N // 16) % tiles or tiles not in (1, 2, 3, 4):
+        raise ValueError("attention_oproj_grouped: heads_per_group in {3, 4} dividing H, tiles in 1..4 dividing N/16")
     if parts.shape[0] < H // hg or parts.shape[2] < N or parts.stride(2) != 1:
         raise ValueError("attention_oproj_grouped: parts must be [>= H/hg, >= 1, >= N]")
     sc = (1.0 / 8.0) if scale is None else scale

@@ -1547,8 +1547,9 @@ extern "C" int dlms_dataflow_decode(const df::Args* args, int grid, hipStream_t 
     DF_CASE(256)
     DF_CASE(768)
     DF_CASE(1024)
-    DF_CASE(1280)
-    DF_CASE(1600)
+    // (d 1280 / 1600 -- GPT-2-large / XL -- were built and oracle-tested in round 4 but measured slower
+    // than launch-per-op, 152 / 306 vs 128.5 / 218 ms per query with 11 / 76 spilled VGPRs
+    // (docs/PERFORMANCE.md round 4); the instantiations are removed)
 #undef DF_CASE
     return (int)hipErrorInvalidValue;
 }

@@ -951,8 +951,7 @@ extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long 
                                       const void* Wp_sl, const float* b_p, void* r_out, int ldr, long long rcs, int M,
                                       int K, int F, int want_cg, int base, hipStream_t stream) {
     if (M <= 0 || M > 8 || F % 16 || F <= 0) return hipErrorInvalidValue;
-    if (nsplit != 0 && nsplit != 1 && !(nsplit == 4 && K <= 1280) && !(nsplit == 5 && K == 1600))
-        return hipErrorInvalidValue;
+    if (nsplit != 0 && nsplit != 1 && (nsplit != 4 || K > 1024)) return hipErrorInvalidValue;
     const int cg = dlms_skinny_mlp_cg(K, M, want_cg);
     if (cg == 0) return hipErrorInvalidValue;
     const bf16_t* Wf = reinterpret_cast<const bf16_t*>(Wfc_sh);
@@ -972,12 +971,10 @@ extern "C" hipError_t dlms_skinny_mlp(const void* x_in, int ldx, int xfix, long 
             if (nsplit == 4) MLP_K(4, 4, 32);
             if (nsplit == 1) MLP_K(1, 4, 32);
             MLP_K(0, 4, 32);
-        case 1280:  // (4 slabs: GPT-2-large's 20 heads in head groups of 5)
-            if (nsplit == 4) MLP_K(4, 5, 40);
+        case 1280:
             if (nsplit == 1) MLP_K(1, 5, 40);
             MLP_K(0, 5, 40);
-        case 1600:  // (5 slabs: GPT-2-XL's 25 heads in head groups of 5)
-            if (nsplit == 5) MLP_K(5, 7, 50);
+        case 1600:
             if (nsplit == 1) MLP_K(1, 7, 50);
             MLP_K(0, 7, 50);
         default: return hipErrorInvalidValue;
@@ -1401,8 +1398,8 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(
 // head (keys split WPH ways, log-sum-exp merge in LDS) and their 2*HG k-blocks of its NT W_o tiles,
 // so the out-projection lands in H / HG slabs instead of H -- with HG = H / 4 exactly the four
 // split-K slabs the fused add+LN kernel already sums (12 slabs cost that kernel ~2 us at batch 1).
-// GPT-2-large / XL (20 / 25 heads): groups of 5 heads, 2 waves per head (a workgroup holds at most
-// 16 waves) -> 4 / 5 slabs for the fused MLP.
+// (Groups of 5 heads at 2 waves per head for GPT-2-large / XL measured slower than the split
+// attention + in-place out-projection: profiles/r5_large_xl_hg5_tiles_ab.jsonl.)
 template <int HG, int NT, int WPH>
 __global__ __launch_bounds__(64 * WPH * HG) void attn_oproj_hg_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
@@ -1544,7 +1541,7 @@ extern "C" hipError_t dlms_attention_oproj_grouped(const void* q, const void* kc
                                                    const int* row_kvlen, int H, int hg, int t_max, int n_slots,
                                                    float scale, const void* wo_sh, int N, int nt, float* part,
                                                    long long split_stride, hipStream_t stream) {
-    if (H < 1 || hg < 1 || H % hg || t_max < 1 || N % 16 || nt < 1 || nt > (hg == 5 ? 10 : 4 * hg) || (N / 16) % nt)
+    if (H < 1 || hg < 1 || H % hg || t_max < 1 || N % 16 || nt < 1 || nt > 4 * hg || (N / 16) % nt)
         return hipErrorInvalidValue;
     const float sl2 = scale * 1.4426950408889634f;
     const dim3 grid(H / hg, (N / 16) / nt);
@@ -1557,7 +1554,6 @@ extern "C" hipError_t dlms_attention_oproj_grouped(const void* q, const void* kc
 #define AOG(HG_, NT_, WPH_) \
     if (hg == HG_ && nt == NT_) { go(attn_oproj_hg_kernel<HG_, NT_, WPH_>, 64 * WPH_ * HG_); return hipGetLastError(); }
     AOG(3, 1, 4) AOG(3, 2, 4) AOG(3, 3, 4) AOG(3, 4, 4) AOG(4, 1, 4) AOG(4, 2, 4) AOG(4, 3, 4) AOG(4, 4, 4)
-    AOG(5, 4, 2) AOG(5, 5, 2) AOG(5, 10, 2)
 #undef AOG
     return hipErrorInvalidValue;
 }

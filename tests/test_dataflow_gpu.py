@@ -63,8 +63,7 @@ def _oracle(cfg, w, outs, prompts, eps=0.05):
 
 @pytest.mark.parametrize("name,T,lens", [("gpt2-tiny", 64, [9]), ("gpt2-tiny", 64, [9, 20]),
                                          ("gpt2", 150, [32]), ("gpt2", 150, [32, 17]),
-                                         ("gpt2-medium", 80, [24]), ("gpt2-large", 80, [24]),
-                                         ("gpt2-xl", 64, [16]), ("gpt2-xl", 64, [16, 5])])
+                                         ("gpt2-medium", 80, [24]), ("gpt2-medium", 80, [24, 7])])
 def test_dataflow_matches_fp32_oracle(name, T, lens):
     """No token differs from the fp32 oracle where its top-1/top-2 margin is decisive; and most
     positions ARE decisive (random-init GPT-2-XL's flatter logits: about 2/3 of them at eps 0.05)."""

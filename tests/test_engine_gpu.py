@@ -108,8 +108,8 @@ def test_fused_mlp_batch1(name, monkeypatch):
     prompts = _prompts(cfg, [13], seed=21)
     fused = HipGPT2Engine(cfg, w, max_batch=1, max_length=64)
     assert fused.fused_mlp and fused.xr is not None
-    # attention fused with the out-projection in head groups: 4 slabs (12 / 16 / 20 heads), 5 (XL's 25)
-    assert fused.ao_groups and fused.ao_slabs == (5 if name == "gpt2-xl" else 4)
+    # batch 1 of 12 / 16 heads: attention fused with the out-projection in 4 head-group slabs
+    assert bool(fused.ao_groups) == (name in ("gpt2", "gpt2-medium"))
     a = fused.generate(prompts)
     assert fused.generate(prompts) == a
     assert HipGPT2Engine(cfg, w, max_batch=1, max_length=64, use_graph=False).generate(prompts) == a

@@ -247,12 +247,10 @@ def test_attention_oproj(M, H, T):
     assert torch.all(parts[:, M:] == 7.0)  # rows >= M untouched
 
 
-@pytest.mark.parametrize("H,hg,tiles", [(12, 3, 3), (12, 3, 1), (16, 4, 4), (16, 4, 2), (12, 4, 3),
-                                        (20, 5, 5), (25, 5, 5), (25, 5, 10), (20, 5, 4)])
+@pytest.mark.parametrize("H,hg,tiles", [(12, 3, 3), (12, 3, 1), (16, 4, 4), (16, 4, 2), (12, 4, 3)])
 @pytest.mark.parametrize("T", [1, 37, 150])
 def test_attention_oproj_grouped(H, hg, tiles, T):
-    """One row, heads in groups of hg: slab g == sum over its heads of attn_h(q) -> bf16 -> @ W_o[:, h]^T
-    (groups of 5: GPT-2-large / XL's 20 / 25 heads, 2 waves per head)."""
+    """One row, heads in groups of hg: slab g == sum over its heads of attn_h(q) -> bf16 -> @ W_o[:, h]^T."""
     ops = _ops()
     N, S = H * 64, 5
     kc, vc = _rand(S, H, T, 64, seed=121), _rand(S, H, T, 64, seed=122)
