@@ -32,7 +32,7 @@ typedef __attribute__((address_space(1))) void ps_glob_void_t;
 #define PS_PAD 32      // LDS row padding (bytes): 8-bank shift per row -> conflict-free fragments
 #define PS_STAGE 4096  // wave-private epilogue staging bytes
 
-template <int EPI, int MT, int NT>
+template <int EPI, int MT, int NT, int KBC = PS_KBC>
 __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __restrict__ A, int lda,
                                                            const bf16_t* __restrict__ Wsh, int M, int N, int K,
                                                            int row_blocks, int split, int col_wgs, GemmEpi ep) {
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
     const int cw = rest / split;
     const int kc = K / split;          // K slice of this block
     const int nkb = kc >> 5;           // its k-blocks
-    const int nch = nkb / PS_KBC;      // register chunks per column tile
+    const int nch = nkb / KBC;      // register chunks per column tile
     const int m0 = rb * BM;
     const int row_bytes = kc * 2 + PS_PAD;
 
@@ -82,15 +82,15 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
     auto frag_ptr = [&](int step, int kb, int t) {
         const int tile = slot + (step / nch) * slots;
         const int cg = tile * NT + t;
-        const int kbi = kb_base + (step % nch) * PS_KBC + kb;
+        const int kbi = kb_base + (step % nch) * KBC + kb;
         return reinterpret_cast<const bf16x8_t*>(Wsh) + ((size_t)cg * nkb_all + kbi) * 64 + lane;
     };
-    bf16x8_t b0[PS_KBC][NT], b1[PS_KBC][NT], b2[PS_KBC][NT], b3[PS_KBC][NT];
+    bf16x8_t b0[KBC][NT], b1[KBC][NT], b2[KBC][NT], b3[KBC][NT];
     // steps past the end re-load the last one (static load counts keep every vmcnt wait counted)
-    auto load = [&](bf16x8_t (&b)[PS_KBC][NT], int step_) {
+    auto load = [&](bf16x8_t (&b)[KBC][NT], int step_) {
         const int step = step_ < nsteps ? step_ : nsteps - 1;
 #pragma unroll
-        for (int kb = 0; kb < PS_KBC; ++kb)
+        for (int kb = 0; kb < KBC; ++kb)
 #pragma unroll
             for (int t = 0; t < NT; ++t) b[kb][t] = *frag_ptr(step, kb, t);
     };
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
             for (int t = 0; t < NT; ++t) acc[i][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     };
 
-    auto compute = [&](const bf16x8_t (&b)[PS_KBC][NT], int step) {
-        const int kb0 = (step % nch) * PS_KBC;
+    auto compute = [&](const bf16x8_t (&b)[KBC][NT], int step) {
+        const int kb0 = (step % nch) * KBC;
         unsigned int swl = 0, swl2 = 0;
         if constexpr (EPI == PS_ARGMAX) {
             // one seen-bitmap word per lane per chunk (unconditional: a static load count keeps the
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
             }
         }
 #pragma unroll
-        for (int kb = 0; kb < PS_KBC; ++kb) {
+        for (int kb = 0; kb < KBC; ++kb) {
             bf16x8_t a[MT];
 #pragma unroll
             for (int i = 0; i < MT; ++i)
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
     }
 }
 
-template <int EPI, int MT, int NT>
+template <int EPI, int MT, int NT, int KBC = PS_KBC>
 static hipError_t launch_ps(const void* A, int lda, const void* W, int M, int N, int K, int split, int col_wgs,
                             const GemmEpi& ep, hipStream_t stream) {
     const int kc = K / split;
@@ -294,12 +294,12 @@ static hipError_t launch_ps(const void* A, int lda, const void* W, int M, int N,
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ps_kernel<EPI, MT, NT>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ps_kernel<EPI, MT, NT, KBC>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((gemm_ps_kernel<EPI, MT, NT>), dim3(row_blocks * split * col_wgs), dim3(64 * PS_NW), lds, stream,
+    hipLaunchKernelGGL((gemm_ps_kernel<EPI, MT, NT, KBC>), dim3(row_blocks * split * col_wgs), dim3(64 * PS_NW), lds, stream,
                        reinterpret_cast<const bf16_t*>(A), lda, reinterpret_cast<const bf16_t*>(W), M, N, K, row_blocks,
                        split, col_wgs, ep);
     return hipGetLastError();
@@ -312,6 +312,15 @@ extern "C" hipError_t dlms_gemm_ps(int epi, const void* A, int lda, const void* 
     if (M <= 0 || N % (16 * nt) || split < 1 || K % split || (K / split) % (32 * PS_KBC) || col_wgs < 1)
         return hipErrorInvalidValue;
     if (epi != PS_PARTIAL && split != 1) return hipErrorInvalidValue;
+    {  // EXPERIMENT: the argmax LM head on 8-k-block register chunks (16 KiB in flight per wave)
+        static int kbc8 = -1;
+        if (kbc8 < 0) {
+            const char* e = getenv("DLMS_PS_KBC_EXP");
+            kbc8 = (e && e[0] == '8') ? 1 : 0;
+        }
+        if (kbc8 && epi == PS_ARGMAX && mt == 4 && nt == 2 && (K / split) % (32 * 8) == 0)
+            return launch_ps<PS_ARGMAX, 4, 2, 8>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream);
+    }
 #define PS_GEO(E)                                                                                         \
     if (mt == 2 && nt == 1) return launch_ps<E, 2, 1>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
     if (mt == 2 && nt == 2) return launch_ps<E, 2, 2>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
