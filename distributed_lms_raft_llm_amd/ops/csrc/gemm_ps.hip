@@ -32,7 +32,7 @@ typedef __attribute__((address_space(1))) void ps_glob_void_t;
 #define PS_PAD 32      // LDS row padding (bytes): 8-bank shift per row -> conflict-free fragments
 #define PS_STAGE 4096  // wave-private epilogue staging bytes
 
-template <int EPI, int MT, int NT, int KBC = PS_KBC>
+template <int EPI, int MT, int NT, int KBC = PS_KBC, int NB = 0>
 __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __restrict__ A, int lda,
                                                            const bf16_t* __restrict__ Wsh, int M, int N, int K,
                                                            int row_blocks, int split, int col_wgs, GemmEpi ep) {
@@ -85,7 +85,6 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
         const int kbi = kb_base + (step % nch) * KBC + kb;
         return reinterpret_cast<const bf16x8_t*>(Wsh) + ((size_t)cg * nkb_all + kbi) * 64 + lane;
     };
-    bf16x8_t b0[KBC][NT], b1[KBC][NT], b2[KBC][NT], b3[KBC][NT];
     // steps past the end re-load the last one (static load counts keep every vmcnt wait counted)
     auto load = [&](bf16x8_t (&b)[KBC][NT], int step_) {
         const int step = step_ < nsteps ? step_ : nsteps - 1;
@@ -210,6 +209,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
             int srow = m0 + 16 * (fr >> 2) + 4 * g + (fr & 3);
             srow = srow < M ? srow : M - 1;
             swl = ep.seen[(size_t)srow * ep.seen_words + ((tile * NT * 16 + ep.col_offset) >> 5)];
+            static_assert(NT <= 2, "a tile's columns share one seen word per row");
             if constexpr (MT > 4) {  // a lane's word covers row tiles 0..3; tiles 4..7 take a second one
                 static_assert(MT <= 8, "two seen words per lane cover at most 8 row tiles");
                 int srow2 = m0 + 16 * ((fr >> 2) + 4) + 4 * g + (fr & 3);
@@ -232,44 +232,27 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
     };
 
     // register ring of weight chunks: NBUF-1 chunks in flight behind the one being computed.  The
-    // argmax variant at 64 x 32 wave tiles double-buffers: its running keys leave no registers for a
-    // deeper ring (3- and 4-deep rings spill there and ran 2.5x slower, profiles/r2_gemm_ps_vs_tiled.log).
-    constexpr int NBUF = (EPI == PS_ARGMAX && MT * NT >= 8) ? 2 : 4;
+    // argmax variant at 64 x 32 wave tiles double-buffers by default: its running keys leave no
+    // registers for a deeper ring of 4-k-block chunks (3- and 4-deep rings spill there and ran 2.5x
+    // slower, profiles/r2_gemm_ps_vs_tiled.log)
+    constexpr int NBUF = NB > 0 ? NB : ((EPI == PS_ARGMAX && MT * NT >= 8) ? 2 : 4);
+    static_assert(NBUF >= 2 && NBUF <= 4, "2..4 register chunks");
+    bf16x8_t b[NBUF][KBC][NT];
     if (nsteps > 0) {
-        load(b0, 0);
-        if constexpr (NBUF == 4) {
-            load(b1, 1);
-            load(b2, 2);
-        }
+#pragma unroll
+        for (int j = 0; j < NBUF - 1; ++j) load(b[j], j);
     }
     // the activation panel: every wave's LDS-DMA landed, then all waves may read it
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if constexpr (NBUF == 4) {
-        for (int step = 0; step < nsteps; step += 4) {
-            load(b3, step + 3);
-            compute(b0, step);
-            if (step + 1 >= nsteps) break;
-            load(b0, step + 4);
-            compute(b1, step + 1);
-            if (step + 2 >= nsteps) break;
-            load(b1, step + 5);
-            compute(b2, step + 2);
-            if (step + 3 >= nsteps) break;
-            load(b2, step + 6);
-            compute(b3, step + 3);
-        }
-    } else {
-        for (int step = 0; step < nsteps; step += 2) {
-            load(b1, step + 1);
-            compute(b0, step);
-            if (step + 1 >= nsteps) break;
-            load(b0, step + 2);
-            compute(b1, step + 1);
+    for (int step = 0; step < nsteps; step += NBUF) {
+#pragma unroll
+        for (int j = 0; j < NBUF; ++j) {  // (compile-time buffer indices: the ring stays in registers)
+            if (j > 0 && step + j >= nsteps) break;
+            load(b[(j + NBUF - 1) % NBUF], step + j + NBUF - 1);
+            compute(b[j], step + j);
         }
     }
-    (void)b2;
-    (void)b3;
 
     if constexpr (EPI == PS_ARGMAX) {
         // per-row max over the 16 column lanes, one key per (row, wave slot)
@@ -285,7 +268,7 @@ __global__ __launch_bounds__(64 * PS_NW) void gemm_ps_kernel(const bf16_t* __res
     }
 }
 
-template <int EPI, int MT, int NT, int KBC = PS_KBC>
+template <int EPI, int MT, int NT, int KBC = PS_KBC, int NB = 0>
 static hipError_t launch_ps(const void* A, int lda, const void* W, int M, int N, int K, int split, int col_wgs,
                             const GemmEpi& ep, hipStream_t stream) {
     const int kc = K / split;
@@ -294,33 +277,30 @@ static hipError_t launch_ps(const void* A, int lda, const void* W, int M, int N,
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ps_kernel<EPI, MT, NT, KBC>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ps_kernel<EPI, MT, NT, KBC, NB>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((gemm_ps_kernel<EPI, MT, NT, KBC>), dim3(row_blocks * split * col_wgs), dim3(64 * PS_NW), lds, stream,
+    hipLaunchKernelGGL((gemm_ps_kernel<EPI, MT, NT, KBC, NB>), dim3(row_blocks * split * col_wgs), dim3(64 * PS_NW), lds, stream,
                        reinterpret_cast<const bf16_t*>(A), lda, reinterpret_cast<const bf16_t*>(W), M, N, K, row_blocks,
                        split, col_wgs, ep);
     return hipGetLastError();
 }
 
-// Geometry: mt = 16-row tiles per block (2 or 4), nt = 16-column groups per wave (1 or 2),
+// Geometry: mt = 16-row tiles per block (2 or 4; 5 for the argmax), nt = 16-column groups per wave (1 or 2),
 // col_wgs = column workgroups (each 8 wave slots of nt groups; tiles beyond the slots loop).
 extern "C" hipError_t dlms_gemm_ps(int epi, const void* A, int lda, const void* Wsh, int M, int N, int K, int split,
                                    int mt, int nt, int col_wgs, const GemmEpi* ep, hipStream_t stream) {
     if (M <= 0 || N % (16 * nt) || split < 1 || K % split || (K / split) % (32 * PS_KBC) || col_wgs < 1)
         return hipErrorInvalidValue;
     if (epi != PS_PARTIAL && split != 1) return hipErrorInvalidValue;
-    {  // EXPERIMENT: the argmax LM head on 8-k-block register chunks (16 KiB in flight per wave)
-        static int kbc8 = -1;
-        if (kbc8 < 0) {
-            const char* e = getenv("DLMS_PS_KBC_EXP");
-            kbc8 = (e && e[0] == '8') ? 1 : 0;
-        }
-        if (kbc8 && epi == PS_ARGMAX && mt == 4 && nt == 2 && (K / split) % (32 * 8) == 0)
-            return launch_ps<PS_ARGMAX, 4, 2, 8>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream);
-    }
+    // the argmax LM head (64 x 32 wave tiles): 8-k-block register chunks, double-buffered -- 16 KiB
+    // of weights in flight per wave instead of 8 (232 VGPRs, no scratch): M = 512 67.5 -> 64.0 us,
+    // M = 1024 107.9 -> 99.7 us (profiles/r5_lmhead_kbc_ab.jsonl; 6-k-block chunks x 3 buffers and
+    // 64 x 64 wave tiles on 4-k-block chunks measured 68.2 / 64.1 us, both with spills)
+    if (epi == PS_ARGMAX && mt == 4 && nt == 2 && (K / split) % (32 * 8) == 0)
+        return launch_ps<PS_ARGMAX, 4, 2, 8, 2>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream);
 #define PS_GEO(E)                                                                                         \
     if (mt == 2 && nt == 1) return launch_ps<E, 2, 1>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \
     if (mt == 2 && nt == 2) return launch_ps<E, 2, 2>(A, lda, Wsh, M, N, K, split, col_wgs, *ep, stream); \

@@ -532,11 +532,12 @@ def test_gemm_ps_qkv(M):
 
 
 @pytest.mark.parametrize("M,K,mt", [(3, 768, 0), (64, 768, 0), (300, 768, 5), (512, 768, 0), (512, 768, 5),
-                                    (512, 1024, 0), (1024, 1024, 0), (256, 1280, 0)])
+                                    (512, 1024, 0), (1024, 1024, 0), (256, 1280, 0), (77, 1280, 2)])
 def test_gemm_ps_argmax_matches_tiled(M, K, mt):
     """Same keys as the tiled LM head's fused penalty + argmax (identical per-element sums are not
     required: compare the decoded token wherever the fp32 top-2 margin is clear); K > 1008 (GPT-2
-    medium and wider) takes 32-row panels so the panel fits in LDS."""
+    medium and wider) takes 32-row panels so the panel fits in LDS.  64-row panels (K = 768) run
+    the 8-k-block register chunks; 80- and 32-row panels the 4-k-block ones."""
     ops = _ops()
     V = 50257
     Vp = 50304
@@ -546,7 +547,7 @@ def test_gemm_ps_argmax_matches_tiled(M, K, mt):
                          dtype=torch.int64).to(torch.int32).to(DEV)
     seen &= 0x01010101  # ~1/8 of the vocabulary penalised
     geo = ops.gemm_ps_geometry(M, Vp, ops.EPI_ARGMAX, K=K)
-    if mt:  # the 80-row panel (two seen-bitmap words per lane), not the default
+    if mt:  # the 80-row panel (two seen-bitmap words per lane) / 32-row panels, not the default
         geo = (mt, geo[1], max(1, 256 // -(-M // (16 * mt))))
     keys = torch.zeros(M, 8 * geo[2], dtype=torch.int64, device=DEV)
     ops.gemm_ps(h, ops.shuffle_weight(w), ops.EPI_ARGMAX, argmax_out=keys, seen=seen, vocab=V, penalty=1.2,
