@@ -65,6 +65,7 @@ def _client_main(conn):
     import grpc
 
     from distributed_lms_raft_llm_amd import wire
+    from distributed_lms_raft_llm_amd.lms.service import MSG_TUTOR_BUSY as busy_msg
     from distributed_lms_raft_llm_amd.wire import pb
 
     async def run(cfg):
@@ -85,6 +86,8 @@ def _client_main(conn):
                 r = await stubs[k % len(stubs)].GetLLMAnswer(pb.QueryRequest(token=tok, query=q),
                                                              timeout=cfg["timeout"])
                 ok, n = bool(r.success), len(r.response)
+                if r.response == busy_msg:  # the LMS's answer when every tutoring replica refused (load)
+                    ok, n = False, "BUSY"
             except grpc.RpcError as e:
                 ok, n = False, e.code().name
             out["n"] -= 1
@@ -425,6 +428,10 @@ def main():
                 "sent_in_window": len(win), "ok": len(ok), "failed": len(win) - len(ok),
                 "fail_codes": {c: sum(1 for r in win if not r[2] and r[3] == c)
                                for c in sorted({r[3] for r in win if not r[2]})},
+                # how fast each failure kind came back (admission control: RESOURCE_EXHAUSTED / BUSY
+                # should return in milliseconds, a deadline in --timeout seconds)
+                "fail_p50_ms": {c: round(pct([r[1] for r in win if not r[2] and r[3] == c], 0.5), 1)
+                                for c in sorted({r[3] for r in win if not r[2]})},
                 "p50_ms": round(pct(lat, 0.5), 1) if lat else None, "p99_ms": round(pct(lat, 0.99), 1) if lat else None,
                 "mean_ms": round(statistics.mean(lat), 1) if lat else None,
                 "inflight_mean": round(statistics.mean(infl), 1) if infl else 0,
