@@ -521,15 +521,17 @@ class HipGPT2Engine:
                     else dict(out_bf16=r.h))
         return r
 
-    def _attn_in(self, r: "_Rows", li: int):
-        """LN1 (folding the pending residual update) -> QKV GEMM (+ K/V scattered into the cache)."""
+    def _attn_in(self, r: "_Rows", li: int, ln_done: bool = False):
+        """LN1 (folding the pending residual update) -> QKV GEMM (+ K/V scattered into the cache).
+        ``ln_done``: r.h already holds LN1 of the row (layer 0 after a fused ``decode_update``)."""
         if self._skip(r) in ("gemm", "ln", "all"):  # timing-only experiment: see __init__
             if self._skip(r) == "ln":
                 self._attn_in_gemm_only(r, li)
             return
         lw, eps, pend = self.w.layers[li], self.cfg.layer_norm_epsilon, r.pend
         kc, vc = self.kv[li, 0], self.kv[li, 1]
-        ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
+        if not ln_done:
+            ops.add_layernorm(r.x, lw.ln1_g, lw.ln1_b, eps, parts=pend[0], nsplit=pend[1], bias=pend[2], **r.ln_out)
         if self.w.fp8:
             ops.gemm(r.h8, lw.w_qkv8, ops.EPI_QKV, bias=lw.b_qkv, q_out=r.q, k_cache=kc, v_cache=vc,
                      row_slot=r.row_slot, row_pos=r.row_pos, a_scale=r.hsc, w_scale=lw.s_qkv)
@@ -609,9 +611,11 @@ class HipGPT2Engine:
         self._final_ln(r, final_h)
 
     def _lm_head_and_update(self, hidden: torch.Tensor | None, B: int, penalty: float, seen: torch.Tensor | None = None,
-                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0):
+                            hscale: torch.Tensor | None = None, slot_map: torch.Tensor | None = None, lo: int = 0,
+                            ln1_out: torch.Tensor | None = None):
         """LM head with the fused penalty + argmax on ``hidden`` (bf16, or e4m3 with ``hscale``),
-        then the greedy bookkeeping.  Rows map to slots [lo, lo + B) or through ``slot_map``."""
+        then the greedy bookkeeping.  Rows map to slots [lo, lo + B) or through ``slot_map``.
+        ``ln1_out`` (rows [lo, lo + B)): the update also writes layer 0's LN1 of the new rows there."""
         cfg = self.cfg
         hi = lo + B
         seen_rows = self.seen[lo:hi] if seen is None else seen
@@ -634,9 +638,12 @@ class HipGPT2Engine:
         else:
             keys = self._gather_keys(B, P)
         if slot_map is None:
+            l0 = self.w.layers[0]
             ops.decode_update(keys, self.lens[lo:hi], self.finished[lo:hi], self.out_tokens[lo:hi],
                               self.seen[lo:hi], self.cur_tok[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi],
-                              self.w.wte, self.w.wpe, self.x[lo:hi], cfg.eos_token_id, self.max_length)
+                              self.w.wte, self.w.wpe, self.x[lo:hi], cfg.eos_token_id, self.max_length,
+                              ln=(l0.ln1_g, l0.ln1_b, cfg.layer_norm_epsilon) if ln1_out is not None else None,
+                              h=ln1_out)
         else:
             ops.decode_update(keys, self.lens, self.finished, self.out_tokens, self.seen, self.cur_tok, self.cur_pos,
                               self.cur_kvlen, self.w.wte, self.w.wpe, self.x, cfg.eos_token_id, self.max_length,
@@ -656,17 +663,23 @@ class HipGPT2Engine:
         r.pidx = lo // max(1, hi - lo)
         return r
 
-    def _part_step(self, r: "_Rows", lo: int, penalty: float):
-        """The whole decode step for one row range (rows are independent sequences)."""
+    def _part_step(self, r: "_Rows", lo: int, penalty: float, h_ready: bool = False):
+        """The whole decode step for one row range (rows are independent sequences).  bf16: the
+        step's ``decode_update`` also writes layer 0's LN1 of the new rows into r.h, so a step that
+        follows one in the same graph replay (``h_ready``) skips that launch."""
+        # (decode per 1024-query generation 152.9 / 153.1 ms against 154.3 / 154.4 with the launch,
+        # profiles/r5_fused_ln1_ab.jsonl; tokens bit-identical: test_kernels_gpu.py::
+        # test_decode_update_fused_ln1_is_bit_identical, test_engine_gpu.py multi-step tests)
+        fuse = not self.w.fp8 and not self._timing_skip
         for li in range(len(self.w.layers)):
-            self._attn_in(r, li)
+            self._attn_in(r, li, ln_done=li == 0 and h_ready and fuse)
             self._attn(r, li)
             self._attn_out_mlp(r, li)
         self._final_ln(r, r.h)
         if self.w.fp8:
             self._lm_head_and_update(r.h8, r.M, penalty, hscale=r.hsc, lo=lo)
         else:
-            self._lm_head_and_update(r.h, r.M, penalty, lo=lo)
+            self._lm_head_and_update(r.h, r.M, penalty, lo=lo, ln1_out=r.h if fuse else None)
 
     def _decode_step_overlap(self, B: int, penalty: float, nsteps: int = 1):
         """Decode step as ``overlap_parts`` row ranges on as many HIP streams (one hardware queue
@@ -691,7 +704,7 @@ class HipGPT2Engine:
                 for i in range(nsteps):
                     # (fresh row state per step: _Rows carries the residual update pending
                     # between layers, which the last layer of a step leaves set)
-                    self._part_step(r if i == 0 else self._part_rows(lo, lo + step), lo, penalty)
+                    self._part_step(r if i == 0 else self._part_rows(lo, lo + step), lo, penalty, h_ready=i > 0)
         for s in streams[1:]:
             cur.wait_stream(s)
 

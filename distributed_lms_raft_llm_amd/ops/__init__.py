@@ -144,7 +144,7 @@ def _bind(L):
         "dlms_tile_attention": [P, I, P, P, P, P, P, I, P, I, I, I, I, F, P],
         "dlms_embed": [P, P, P, P, P, I, I, I, I, I, P],
         "dlms_decode_update": [P, I, ctypes.c_longlong, ctypes.c_longlong, P, P, P, P, I, P, I, P, P, P, P, P, P, I, I,
-                               I, I, I, I, I, P],
+                               I, I, I, I, I, P, P, F, P, I, P],
         "dlms_argmax_reduce": [P, I, ctypes.c_longlong, P, I, P],
         "dlms_seen_set": [P, P, I, P, I, I, P],
         "dlms_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, I, I, P],
@@ -631,10 +631,12 @@ def seen_set(seen: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor):
 
 
 def decode_update(keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok, cur_pos, cur_kvlen, wte, wpe, x,
-                  eos: int, t_max: int, slot_map: torch.Tensor | None = None):
+                  eos: int, t_max: int, slot_map: torch.Tensor | None = None, ln=None, h: torch.Tensor | None = None):
     """keys: int64 [R, P] (row-major partial keys) or a transposed view [P, R].T (gathered per-rank
     keys); the token of row i is the argmax over its P keys and updates sequence slot
-    ``slot_map[i]`` (default: slot i)."""
+    ``slot_map[i]`` (default: slot i).  ``ln=(gamma, beta, eps)`` + ``h``: also write
+    bf16(LN(x_new) * gamma + beta) of every updated slot into ``h`` (layer 0's LN1, bit-identical to
+    ``add_layernorm`` on the stored row)."""
     if keys.dtype != torch.int64 or keys.device.type != "cuda" or keys.dim() != 2:
         raise ValueError("decode_update: keys must be a 2-D int64 GPU tensor")
     B, P = keys.shape
@@ -655,11 +657,25 @@ def decode_update(keys: torch.Tensor, lens, finished, out_tokens, seen, cur_tok,
     D = wte.shape[1]
     if out_tokens.shape[0] < nslots or x.shape[0] < nslots or x.shape[1] < D or seen.shape[0] < nslots:
         raise ValueError("decode_update: buffers too small")
+    g = b = None
+    eps = 0.0
+    if (ln is None) != (h is None):
+        raise ValueError("decode_update: ln and h go together")
+    if h is not None:
+        g, b, eps = ln
+        _req(h, torch.bfloat16, "h", 2)
+        for t, n in ((g, "gamma"), (b, "beta")):
+            _req(t, torch.float32, n, 1)
+            if t.numel() < D or not t.is_contiguous():
+                raise ValueError(f"decode_update: {n} must be contiguous [D]")
+        if h.shape[0] < nslots or h.shape[1] < D or h.stride(1) != 1 or h.stride(0) % 4 or h.data_ptr() % 8:
+            raise ValueError("decode_update: h must be [>= slots, >= D] bf16 rows, 8-B aligned")
     _check(lib().dlms_decode_update(_p(keys), P, keys.stride(0), keys.stride(1), _p(slot_map), _p(lens), _p(finished),
                                     _p(out_tokens),
                                     out_tokens.stride(0), _p(seen), seen.stride(0), _p(cur_tok), _p(cur_pos),
                                     _p(cur_kvlen), _p(wte), _p(wpe), _p(x), x.stride(0), B, D, eos, t_max,
-                                    lens.numel(), wte.shape[0], _stream()),
+                                    lens.numel(), wte.shape[0], _p(g), _p(b), float(eps), _p(h),
+                                    h.stride(0) if h is not None else 0, _stream()),
            "dlms_decode_update")
 
 

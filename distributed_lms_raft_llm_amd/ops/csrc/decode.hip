@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
     if (lane == 0) out[b] = best;
 }
 
-#define DU_MAXC 4  // 16-B embedding chunks per lane: D <= 64 * 4 * 8 = 2048
+#define DU_MAXV4 8  // float4 chunks of the new row per lane: D <= 64 * 8 * 4 = 2048
 
 // One wave per live sequence b.
 //   keys(b, p)   packed (ordered value, ~index) argmax keys: the LM head's per-column-tile
@@ -75,7 +75,10 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
                                                             int* cur_pos, int* cur_kvlen,
                                                             const bf16_t* __restrict__ wte,
                                                             const bf16_t* __restrict__ wpe, float* x, int ldx, int B,
-                                                            int D, int eos, int t_max, int n_slots, int V) {
+                                                            int D, int eos, int t_max, int n_slots, int V,
+                                                            const float* __restrict__ ln_g,
+                                                            const float* __restrict__ ln_b, float eps, bf16_t* h,
+                                                            int ldh) {
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= B) return;
@@ -88,12 +91,14 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
     int pos = fin ? len0 - 1 : live_len;  // (length after this step) - 1
     pos = pos < 0 ? 0 : (pos < t_max - 1 ? pos : t_max - 1);
     const int last_tok = fin ? out_tokens[(size_t)b * max_len + (len0 > 0 ? len0 - 1 : 0)] : 0;
-    const int nch = D >> 3;
-    uint4 pe[DU_MAXC];
+    // the row in float4 chunks c = lane + 64 j -- add_layernorm_kernel's partition, so the fused
+    // LayerNorm below computes exactly what that kernel would on the stored row
+    const int nv = D >> 2;
+    uint2 pe[DU_MAXV4];
 #pragma unroll
-    for (int u = 0; u < DU_MAXC; ++u) {
-        const int c = lane + 64 * u;
-        pe[u] = c < nch ? *reinterpret_cast<const uint4*>(wpe + (size_t)pos * D + c * 8) : make_uint4(0u, 0u, 0u, 0u);
+    for (int j = 0; j < DU_MAXV4; ++j) {
+        const int c = lane + 64 * j;
+        pe[j] = c < nv ? *reinterpret_cast<const uint2*>(wpe + (size_t)pos * D + c * 4) : make_uint2(0u, 0u);
     }
     const unsigned long long best = wave_key_max(keys, i, nparts, sb, sp, lane);
 
@@ -118,16 +123,45 @@ __global__ __launch_bounds__(256) void decode_update_kernel(const unsigned long 
         cur_kvlen[b] = pos + 1;
     }
     const bf16_t* a = wte + (size_t)tok * D;
-    float* o = x + (size_t)b * ldx;
+    float4* o = reinterpret_cast<float4*>(x + (size_t)b * ldx);
+    float4 v[DU_MAXV4];
 #pragma unroll
-    for (int u = 0; u < DU_MAXC; ++u) {
-        const int c = lane + 64 * u;
-        if (c >= nch) continue;
-        float fa[8], fb[8];
-        unpack8(*reinterpret_cast<const uint4*>(a + c * 8), fa);
-        unpack8(pe[u], fb);
-        reinterpret_cast<float4*>(o + c * 8)[0] = make_float4(fa[0] + fb[0], fa[1] + fb[1], fa[2] + fb[2], fa[3] + fb[3]);
-        reinterpret_cast<float4*>(o + c * 8)[1] = make_float4(fa[4] + fb[4], fa[5] + fb[5], fa[6] + fb[6], fa[7] + fb[7]);
+    for (int j = 0; j < DU_MAXV4; ++j) {
+        const int c = lane + 64 * j;
+        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c >= nv) continue;
+        const uint2 e = *reinterpret_cast<const uint2*>(a + c * 4);
+        v[j] = make_float4(bf16_to_f32((bf16_t)(e.x & 0xffffu)) + bf16_to_f32((bf16_t)(pe[j].x & 0xffffu)),
+                           bf16_to_f32((bf16_t)(e.x >> 16)) + bf16_to_f32((bf16_t)(pe[j].x >> 16)),
+                           bf16_to_f32((bf16_t)(e.y & 0xffffu)) + bf16_to_f32((bf16_t)(pe[j].y & 0xffffu)),
+                           bf16_to_f32((bf16_t)(e.y >> 16)) + bf16_to_f32((bf16_t)(pe[j].y >> 16)));
+        o[c] = v[j];
+    }
+    if (h == nullptr) return;
+    // layer 0's LN1 of the new row (the overlapped decode step then skips that launch): the same
+    // statistics order as add_layernorm_kernel -- per-lane float4 sums, wave sums, two passes
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < DU_MAXV4; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    const float mean = wave_sum(s) / (float)D;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < DU_MAXV4; ++j) {
+        if (lane + 64 * j < nv) {
+            const float p = v[j].x - mean, q = v[j].y - mean, r = v[j].z - mean, t = v[j].w - mean;
+            ss += (p * p + q * q) + (r * r + t * t);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)D + eps);
+#pragma unroll
+    for (int j = 0; j < DU_MAXV4; ++j) {
+        const int c = lane + 64 * j;
+        if (c >= nv) continue;
+        const float4 g = reinterpret_cast<const float4*>(ln_g)[c], be = reinterpret_cast<const float4*>(ln_b)[c];
+        uint2 pk;
+        pk.x = pack_bf16x2((v[j].x - mean) * rstd * g.x + be.x, (v[j].y - mean) * rstd * g.y + be.y);
+        pk.y = pack_bf16x2((v[j].z - mean) * rstd * g.z + be.z, (v[j].w - mean) * rstd * g.w + be.w);
+        reinterpret_cast<uint2*>(h + (size_t)b * ldh)[c] = pk;
     }
 }
 
@@ -143,12 +177,14 @@ extern "C" hipError_t dlms_decode_update(const unsigned long long* keys, int npa
                                          const int* slot_map, int* lens, int* finished, int* out_tokens, int max_len,
                                          unsigned int* seen, int seen_words, int* cur_tok, int* cur_pos,
                                          int* cur_kvlen, const void* wte, const void* wpe, float* x, int ldx, int B,
-                                         int D, int eos, int t_max, int n_slots, int V, hipStream_t stream) {
-    if (D % 8 != 0 || D > 64 * DU_MAXC * 8 || B <= 0 || nparts <= 0) return hipErrorInvalidValue;
+                                         int D, int eos, int t_max, int n_slots, int V, const float* ln_g,
+                                         const float* ln_b, float eps, void* h, int ldh, hipStream_t stream) {
+    if (D % 8 != 0 || D > 64 * DU_MAXV4 * 4 || B <= 0 || nparts <= 0 || (h && (!ln_g || !ln_b || ldh % 4)))
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(decode_update_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, keys, nparts, sb, sp, slot_map,
                        lens, finished, out_tokens, max_len, seen, seen_words, cur_tok, cur_pos, cur_kvlen,
                        reinterpret_cast<const bf16_t*>(wte), reinterpret_cast<const bf16_t*>(wpe), x, ldx, B, D, eos,
-                       t_max, n_slots, V);
+                       t_max, n_slots, V, ln_g, ln_b, eps, reinterpret_cast<bf16_t*>(h), ldh);
     return hipGetLastError();
 }
 

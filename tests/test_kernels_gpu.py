@@ -373,6 +373,34 @@ def test_embed_and_decode_update():
     torch.testing.assert_close(xb[0], wte[17].float() + wpe[4].float())
 
 
+@pytest.mark.parametrize("D", [768, 1024, 1600])
+def test_decode_update_fused_ln1_is_bit_identical(D):
+    """decode_update's fused layer-0 LN1 (the overlapped step skips that launch on steps 2.. of a
+    graph replay) writes exactly what add_layernorm writes from the stored row -- bit for bit, so
+    the tokens cannot depend on how many steps a replay holds -- and matches the fp32 LayerNorm."""
+    ops = _ops()
+    V, P, B, T = 3000, 256, 37, 150
+    wte, wpe = _bf(V, D, seed=21), _bf(P, D, seed=22)
+    g = torch.randn(D, generator=torch.Generator().manual_seed(23)).to(DEV)
+    b = torch.randn(D, generator=torch.Generator().manual_seed(24)).to(DEV)
+    gk = torch.Generator().manual_seed(25)
+    toks = torch.randint(0, V, (B, 5), generator=gk)
+    keys = ((torch.randint(0, 2**30, (B, 5), generator=gk) << 32) | (~toks & 0xFFFFFFFF)).to(DEV)  # valid ids only
+    lens = torch.randint(1, T - 1, (B,), generator=torch.Generator().manual_seed(26)).to(torch.int32).to(DEV)
+    fin = (torch.arange(B) % 5 == 3).to(torch.int32).to(DEV)
+    out = torch.randint(0, V, (B, T), generator=torch.Generator().manual_seed(27)).to(torch.int32).to(DEV)
+    seen = torch.zeros(B, (V + 31) // 32, dtype=torch.int32, device=DEV)
+    ct, cp, ck = (torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(3))
+    x = torch.zeros(B, D, device=DEV)
+    h = torch.full((B, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops.decode_update(keys, lens, fin, out, seen, ct, cp, ck, wte, wpe, x, eos=V - 1, t_max=T, ln=(g, b, 1e-5), h=h)
+    torch.testing.assert_close(x, wte[ct.long()].float() + wpe[cp.long()].float())
+    ref = torch.empty_like(h)
+    ops.add_layernorm(x.clone(), g, b, 1e-5, out_bf16=ref)
+    assert torch.equal(h.view(torch.int16), ref.view(torch.int16))
+    torch.testing.assert_close(h.float(), torch.nn.functional.layer_norm(x, (D,), g, b, 1e-5), atol=3e-2, rtol=2e-2)
+
+
 def test_bert_embed_pool_cosine():
     ops = _ops()
     V, P, D = 100, 32, 128
