@@ -596,16 +596,17 @@ class HipGPT2Engine:
 
     def _layers(self, x: torch.Tensor, parts: torch.Tensor, h, q, att, ff, row_slot, row_pos, row_kvlen, M: int,
                 final_h: torch.Tensor | None, h8: torch.Tensor | None = None, hsc: torch.Tensor | None = None,
-                tiles: "ops.AttnTiles | None" = None):
+                tiles: "ops.AttnTiles | None" = None, ln0_done: bool = False):
         """All blocks on rows [0, M) of the residual ``x`` (updated in place), then ln_f into
         ``final_h`` (or only the last residual update when ``final_h`` is None).  fp8 weights: the
         LayerNorms emit row-scaled e4m3 into ``h8``/``hsc`` for the W8A8 QKV / c_fc GEMMs, and the
-        ln_f output goes there too (``final_h`` then only says whether it is wanted)."""
+        ln_f output goes there too (``final_h`` then only says whether it is wanted).  ``ln0_done``:
+        h already holds layer 0's LN1 (fused ``decode_update``)."""
         r = self._rows(x, parts, h, q, att, ff, row_slot, row_pos, row_kvlen, M, h8, hsc, tiles)
         if tiles is not None:
             r.split_fixed = self.prefill_split
         for li in range(len(self.w.layers)):
-            self._attn_in(r, li)
+            self._attn_in(r, li, ln_done=li == 0 and ln0_done)
             self._attn(r, li)
             self._attn_out_mlp(r, li)
         self._final_ln(r, final_h)
@@ -902,23 +903,28 @@ class HipGPT2Engine:
             self._all_reduce_i64(acc_all)
             xin = acc_all[:, :B]
 
-    def _decode_step(self, B: int, penalty: float, nsteps: int = 1):
+    def _decode_step(self, B: int, penalty: float, nsteps: int = 1, h_ready: bool = False):
+        """One decode step (``nsteps`` back to back).  ``h_ready``: the previous step of the same
+        graph replay ran the tiled path below, whose ``decode_update`` left layer 0's LN1 in h."""
         if nsteps > 1:
             if self._overlap_ok(B) and not self._small_ok(B):
                 return self._decode_step_overlap(B, penalty, nsteps)
-            for _ in range(nsteps):
-                self._decode_step(B, penalty)
+            for i in range(nsteps):
+                self._decode_step(B, penalty, h_ready=i > 0)
             return
         if self._small_ok(B):
             return self._decode_step_small(B, penalty)
         if self._overlap_ok(B):
             return self._decode_step_overlap(B, penalty)
+        # (batch 256: 84.9 / 84.9 ms per query against 85.8 / 86.4 with the launch; batch 32 within
+        # box noise -- profiles/r5_fused_ln1_tiled_ab.jsonl)
+        fuse = not self.w.fp8 and not self._timing_skip
         self._layers(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
-                     self.cur_kvlen[:B], B, final_h=self.h[:B], h8=self.h8, hsc=self.hsc)
+                     self.cur_kvlen[:B], B, final_h=self.h[:B], h8=self.h8, hsc=self.hsc, ln0_done=h_ready and fuse)
         if self.w.fp8:
             self._lm_head_and_update(self.h8[:B], B, penalty, hscale=self.hsc[:B])
         else:
-            self._lm_head_and_update(self.h[:B], B, penalty)
+            self._lm_head_and_update(self.h[:B], B, penalty, ln1_out=self.h[:B] if fuse else None)
 
     def _graph_for(self, B: int, penalty: float, nsteps: int = 1) -> torch.cuda.CUDAGraph:
         key = (B, float(penalty), nsteps)
