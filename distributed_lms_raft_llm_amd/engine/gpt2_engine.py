@@ -1169,6 +1169,33 @@ class HipGPT2Engine:
             else:
                 self._decode_step(B, repetition_penalty)
 
+    @torch.no_grad()
+    def warm_decode_graphs(self, repetition_penalty: float = 1.2, max_batch: int | None = None) -> tuple[int, float]:
+        """Capture the decode-step graphs ``decode()`` would capture on first use (one step and one
+        replay's worth of steps per batch bucket up to ``max_batch``; the dataflow buckets need none)
+        so a server's first burst of queries does not pay the captures.  Returns (graphs, seconds)."""
+        if not self.use_graph:
+            return 0, 0.0
+        t0 = time.perf_counter()
+        cap = min(self.max_batch, max_batch or self.max_batch)
+        n, B = 0, 1
+        while True:
+            B = min(_bucket(B), self.max_batch)
+            if B > cap:
+                break
+            if not self._df_ok(B):
+                self._graph_for(B, repetition_penalty)
+                n += 1
+                kg = self._steps_per_graph_for(B)
+                if kg > 1:
+                    self._graph_for(B, repetition_penalty, kg)
+                    n += 1
+            if B >= self.max_batch:
+                break
+            B += 1
+        torch.cuda.synchronize(self.device)
+        return n, time.perf_counter() - t0
+
     def _steps_per_graph_for(self, B: int) -> int:
         """Decode steps per graph replay for a batch bucket (DLMS_STEPS_PER_GRAPH[_SMALL])."""
         overlapped = self._overlap_ok(B) and not self._small_ok(B)

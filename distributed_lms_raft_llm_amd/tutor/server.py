@@ -398,6 +398,9 @@ def main(argv=None):
     ap.add_argument("--frontends", type=int, default=4,
                     help="gRPC front-end processes sharing the port (tutor/frontend.py); 0 = serve gRPC in "
                          "this process (--frontend)")
+    ap.add_argument("--warm-batch", type=int, default=1024,
+                    help="capture the decode graphs of every batch bucket up to this size before serving, so "
+                         "the first burst of queries does not pay them (0 = capture on first use)")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     args, _ = parse_with_config(ap, argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
@@ -443,6 +446,9 @@ def main(argv=None):
         eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights,
                           weight_dtype=args.weight_dtype)
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
+    if args.warm_batch > 0 and hasattr(eng, "warm_decode_graphs"):  # (single-GPU engines; not a TP proxy)
+        n, secs = eng.warm_decode_graphs(args.repetition_penalty, args.warm_batch)
+        log.info("captured %d decode graphs (batch buckets <= %d) in %.1f s", n, args.warm_batch, secs)
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
     if pool is not None and hasattr(eng, "admit"):
         srv = PooledTutoringServer(eng, pool, args.max_length, args.repetition_penalty, chunk=args.chunk,

@@ -212,6 +212,22 @@ def test_multi_step_graph_equals_single_step(monkeypatch):
     assert eng.generate(prompts) == a
 
 
+def test_warm_decode_graphs_covers_first_use():
+    """The server's start-up capture (``warm_decode_graphs``) leaves nothing for the first queries
+    to capture, and the tokens are those of an engine that captured on first use."""
+    from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [5 + (3 * i) % 20 for i in range(10)], seed=41)
+    ref = HipGPT2Engine(cfg, w, max_batch=64, max_length=61).generate(prompts)
+    eng = HipGPT2Engine(cfg, w, max_batch=64, max_length=61)
+    n, secs = eng.warm_decode_graphs(1.2, 64)
+    assert n >= 2 and len(eng._graphs) == n and secs >= 0
+    keys = set(eng._graphs)
+    assert eng.generate(prompts) == ref
+    assert set(eng._graphs) == keys  # every decode graph of the 16-row bucket was already there
+
+
 @pytest.mark.parametrize("batch", [1, 2, 5, 24])
 def test_multi_step_graph_small_paths(batch, monkeypatch):
     """Latency path (fused MLP at 1-2 rows, 4-kernel step at 5) and the tiled step (24 rows) with
