@@ -446,6 +446,282 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
 // counted when the launch is issued, so graph captures count once per capture)
 static std::atomic<long> g_tile_count[4][4];  // [BM 32/64/128/256][BN 64/96/128/256]
 
+// ------------------------------------------------------------------------------------------------
+// Big prefill GEMMs (M >= 16384 packed prompt rows): 256x256 tiles, 8 waves, an 8-phase K loop that
+// keeps LDS-DMA half-tiles in flight ACROSS its barriers (cdna_hip_programming.md §5 "The 256² 8-phase
+// template": counted vmcnt, raw s_barrier, all LDS in one dynamic array, the two wave rows a barrier
+// apart so one row's fragment reads run under the other row's MFMAs).
+//
+// LDS: 2 buffers (even / odd K-tile) x {A rows 0-127, A rows 128-255, W rows 0-127, W rows 128-255}
+// half-tiles of 128 rows x 64 k (128-B rows, 16-B chunks XOR-swizzled by row & 7) = 8 x 16 KiB.
+// A phase computes one 128x128 block quadrant (mq, nq) of one K-tile: every wave its 64x32 piece
+// (rows mq*128 + wr*64, cols nq*128 + wc*32; wr = w >> 2, wc = w & 3): 8 A / 4 W fragment reads
+// (skipped when the previous phase read the same half), 16 MFMAs between two barriers.  Quadrant
+// order (0,0) (0,1) (1,1) (1,0) reads a buffer's halves from LDS last in the order A0, W1, A1, W0
+// (fragments are reused in registers between consecutive phases); each phase issues ONE half-tile
+// (2 DMA instructions per thread) into the half whose last read was the phase before:
+//   ph0 odd.W0 (K-tile 2i+1)  ph1 even.A0 (2i+2)  ph2 even.W1 (2i+2)  ph3 even.A1 (2i+2)
+//   ph4 even.W0 (2i+2)        ph5 odd.A0 (2i+3)   ph6 odd.W1 (2i+3)   ph7 odd.A1 (2i+3)
+// and the waits in ph3 / ph7 (vmcnt(6): the three younger half-tiles stay in flight) retire
+// everything the next buffer's four phases read.  K must be a multiple of 128 (an even number of
+// K-tiles).  It sums every output in the same k order as gemm_tn_kernel, so its results are
+// bit-identical to the 128x128 tiles' (tests/test_kernels_gpu.py).
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm8p_kernel(const bf16_t* __restrict__ A, int lda,
+                                                     const bf16_t* __restrict__ W, int ldw, int M, int N, int K,
+                                                     GemmEpi ep) {
+    constexpr int BM = 256, BN = 256, HALF = 16384, ROWB = 128;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 2, wc = w & 3;
+
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+    const int nsplit = EPI == EPI_PARTIAL ? ep.split_k : 1;
+    const int tiles = tiles_m * tiles_n;
+    const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = bid0 / tiles;
+    const int bid = bid0 - split * tiles;
+    // groups of GROUP_M row tiles x all column tiles (an XCD's workgroups share A / W panels in L2)
+    const int per_group = GROUP_M * tiles_n;
+    const int g = bid / per_group, rg = bid - g * per_group;
+    const int gm0 = g * GROUP_M;
+    const int gsz = tiles_m - gm0 < GROUP_M ? tiles_m - gm0 : GROUP_M;
+    const int m0 = (gm0 + rg % gsz) * BM, n0 = (rg / gsz) * BN;
+    const int k_len = K / nsplit, k_base = split * k_len;
+    const int nk = k_len / 64, niter = nk / 2;
+
+    // DMA sources: thread t of wave w fills pieces w and w + 8 (8 rows x 128 B each) of a half
+    // tile; byte offsets (32 bit: operands < 4 GiB) from A / W, before the k offset
+    unsigned aoff[2][2], woff[2][2];  // [half][piece]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+            const int r = (w + 8 * pc) * 8 + (lane >> 3);
+            const int chunk = (lane & 7) ^ (lane >> 3);
+            int gm = m0 + h * 128 + r;
+            gm = gm < M ? gm : M - 1;
+            aoff[h][pc] = (unsigned)((size_t)gm * lda * 2 + (size_t)k_base * 2 + chunk * 16);
+            woff[h][pc] = (unsigned)((size_t)(n0 + h * 128 + r) * ldw * 2 + (size_t)k_base * 2 + chunk * 16);
+        }
+    const char* Ab = reinterpret_cast<const char*>(A);
+    const char* Wb = reinterpret_cast<const char*>(W);
+    // half-tile slots: buffer b, part q (0 A0, 1 A1, 2 W0, 3 W1)
+    auto issue = [&](int b, int q, int kt) {
+#ifdef G8P_DIAG_NODMA
+        if (kt > 1) return;
+#endif
+        char* dst = smem + (b * 4 + q) * HALF;
+        const int h = q & 1;
+        const unsigned kb = (unsigned)kt * 128u;  // 64 bf16 per K-tile
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+            const char* src = q < 2 ? Ab + aoff[h][pc] + kb : Wb + woff[h][pc] + kb;
+            __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)(dst + (w + 8 * pc) * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4_t acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    bf16x8_t af[4][2], bfr[2][2];
+    const int frow = lane & 15, fk = lane >> 4, fsw = lane & 7;
+
+    auto read_a = [&](int b, int mq) {
+        const char* base = smem + (b * 4 + mq) * HALF + (wr * 64) * ROWB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int coff = ((ks * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i][ks] = *reinterpret_cast<const bf16x8_t*>(base + (i * 16 + frow) * ROWB + coff);
+        }
+    };
+    auto read_w = [&](int b, int nq) {
+        const char* base = smem + (b * 4 + 2 + nq) * HALF + (wc * 32) * ROWB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int coff = ((ks * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bfr[j][ks] = *reinterpret_cast<const bf16x8_t*>(base + (j * 16 + frow) * ROWB + coff);
+        }
+    };
+    auto mfma = [&](int mq, int nq) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[mq * 4 + i][nq * 2 + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bfr[j][ks], acc[mq * 4 + i][nq * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    // prologue: what iteration -1 would have issued -- the even buffer <- K-tile 0 (ph1-ph4) and
+    // odd.A0 / odd.W1 / odd.A1 <- K-tile 1 (ph5-ph7); retire K-tile 0, three halves stay in flight
+    issue(0, 0, 0);
+    issue(0, 3, 0);
+    issue(0, 1, 0);
+    issue(0, 2, 0);
+    issue(1, 0, 1);
+    issue(1, 3, 1);
+    issue(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the two wave rows run one barrier apart (two barriers per phase): row 1's fragment reads
+    // overlap row 0's MFMAs and the other way round on every SIMD (cdna guide, 8-phase template)
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+
+    // a phase: LDS fragment reads -> this phase's DMA -> [the K-tile wait] -> reads land -> barrier
+    // -> 16 MFMAs -> barrier.  A wait sits BEFORE the first barrier of the phase ahead of the reads
+    // it guards: with the rows a barrier apart, the other row passes its own wait before the
+    // barrier this row crosses next (RAW); a half is refilled one phase after its last LDS read,
+    // which both rows retired (lgkmcnt(0)) before the barrier ending that phase (WAR).
+    auto sync1 = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    auto wait_ktile = [&](bool more) {
+        if (more)
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // three younger half-tiles stay in flight
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+
+    for (int it = 0; it < niter; ++it) {
+        const bool more = it + 1 < niter;  // K-tiles 2it+2 / 2it+3 exist
+        const int k0 = 2 * it;
+        // ---- even buffer, K-tile k0 (LDS reads: A0 + W0, W1, A1, W0)
+        read_a(0, 0);
+        read_w(0, 0);
+        issue(1, 2, k0 + 1);  // ph0: odd.W0 (its last read was ph7)
+        sync1();
+        mfma(0, 0);
+        __builtin_amdgcn_s_barrier();
+        read_w(0, 1);
+        if (more) issue(0, 0, k0 + 2);  // ph1: even.A0 (last read ph0)
+        sync1();
+        mfma(0, 1);
+        __builtin_amdgcn_s_barrier();
+        read_a(0, 1);
+        if (more) issue(0, 3, k0 + 2);  // ph2: even.W1 (last read ph1)
+        sync1();
+        mfma(1, 1);
+        __builtin_amdgcn_s_barrier();
+        read_w(0, 0);
+        if (more) issue(0, 1, k0 + 2);  // ph3: even.A1 (last read ph2)
+        wait_ktile(more);                // through ph0: the odd K-tile (read from ph4) has landed
+        sync1();
+        mfma(1, 0);
+        __builtin_amdgcn_s_barrier();
+        // ---- odd buffer, K-tile k0 + 1
+        read_a(1, 0);
+        read_w(1, 0);
+        if (more) issue(0, 2, k0 + 2);  // ph4: even.W0 (last read ph3)
+        sync1();
+        mfma(0, 0);
+        __builtin_amdgcn_s_barrier();
+        read_w(1, 1);
+        if (more) issue(1, 0, k0 + 3);  // ph5: odd.A0 (last read ph4)
+        sync1();
+        mfma(0, 1);
+        __builtin_amdgcn_s_barrier();
+        read_a(1, 1);
+        if (more) issue(1, 3, k0 + 3);  // ph6: odd.W1 (last read ph5)
+        sync1();
+        mfma(1, 1);
+        __builtin_amdgcn_s_barrier();
+        read_w(1, 0);
+        if (more) issue(1, 1, k0 + 3);  // ph7: odd.A1 (last read ph6)
+        wait_ktile(more);                // through ph4: the next even K-tile has landed
+        sync1();
+        mfma(1, 0);
+        __builtin_amdgcn_s_barrier();
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // realign the rows
+
+    // ---------------- epilogue: one 128x128 block quadrant at a time through LDS ----------------
+    // (accumulator element r of tile (i, j) of quadrant (mq, nq): row mq*128 + wr*64 + i*16 +
+    // (lane>>4)*4 + r, column nq*128 + wc*32 + j*16 + (lane&15))
+    constexpr int OB = EPI == EPI_PARTIAL ? 4 : 2;
+    constexpr int SROW = 128 * OB + 16;
+    constexpr int CPR = 128 * OB / 16;
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int nq = 0; nq < 2; ++nq) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int lc = wc * 32 + j * 16 + (lane & 15);
+                const float bv = (EPI != EPI_PARTIAL && ep.bias) ? ep.bias[n0 + nq * 128 + lc] : 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = acc[mq * 4 + i][nq * 2 + j][r] + bv;
+                        if constexpr (EPI == EPI_GELU_TANH) v = gelu_tanh(v);
+                        char* dst = smem + (wr * 64 + i * 16 + (lane >> 4) * 4 + r) * SROW + lc * OB;
+                        if constexpr (OB == 4)
+                            *reinterpret_cast<float*>(dst) = v;
+                        else
+                            *reinterpret_cast<bf16_t*>(dst) = f32_to_bf16(v);
+                    }
+            }
+            __syncthreads();
+            for (int c = tid; c < 128 * CPR; c += 512) {
+                const int lr = c / CPR, ch = c - lr * CPR;
+                const int row = m0 + mq * 128 + lr;
+                if (row >= M) continue;
+                const uint4 val = *reinterpret_cast<const uint4*>(smem + lr * SROW + ch * 16);
+                const int col = n0 + nq * 128 + ch * (16 / OB);
+                if constexpr (EPI == EPI_PARTIAL) {
+                    *reinterpret_cast<uint4*>(reinterpret_cast<float*>(ep.out) + (size_t)split * ep.split_stride +
+                                              (size_t)row * ep.ldo + col) = val;
+                } else if constexpr (EPI == EPI_QKV) {
+                    const int part = col / ep.d_local;
+                    const int within = col - part * ep.d_local;
+                    bf16_t* dst;
+                    if (part == 0) {
+                        dst = ep.q_out + (size_t)row * ep.ldq + within;
+                    } else {
+                        const int head = within >> 6, dim = within & 63;
+                        const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
+                        const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
+                        dst = (part == 1 ? ep.k_cache : ep.v_cache) + ((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim;
+                    }
+                    *reinterpret_cast<uint4*>(dst) = val;
+                } else {
+                    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(ep.out) + (size_t)row * ep.ldo + col) = val;
+                }
+            }
+            __syncthreads();
+        }
+}
+
+template <int EPI>
+static hipError_t launch_gemm8p(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const GemmEpi& ep,
+                                hipStream_t stream) {
+    const int split = EPI == EPI_PARTIAL ? ep.split_k : 1;
+    if (N % 256 != 0 || (K / split) % 128 != 0 || K % split != 0) return hipErrorInvalidValue;
+    const size_t lds = 8 * 16384;  // >= the 128 x (128 x 4 + 16) B staged fp32 epilogue quadrant
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8p_kernel<EPI>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    g_tile_count[3][3].fetch_add(1, std::memory_order_relaxed);
+    const int tiles = ((M + 255) / 256) * (N / 256) * split;
+    hipLaunchKernelGGL(gemm8p_kernel<EPI>, dim3(tiles), dim3(512), lds, stream, reinterpret_cast<const bf16_t*>(A), lda,
+                       reinterpret_cast<const bf16_t*>(W), ldw, M, N, K, ep);
+    return hipGetLastError();
+}
+
+
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN, int MODE = 0>
 static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw, int M, int N, int K,
                                   const GemmEpi& ep, hipStream_t stream) {
@@ -534,6 +810,10 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
     // the forced-tile tests: 24 = both, 25 = GROUPED.  (Round 4's 256x256 / 256x128 mode variants and
     // the one-row-tile LM heads, all measured slower, were removed: profiles/r4_prefill_gemm_modes.jsonl,
     // r4_lmhead_tiles_m512.jsonl.)
+    if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
+        if (id == 26 && N % 256 == 0 && (K / (EPI == EPI_PARTIAL ? ep.split_k : 1)) % 128 == 0)
+            return launch_gemm8p<EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    }
     if constexpr (IN == IN_BF16) {
         if (N % 128 == 0) {
             switch (id) {
@@ -565,6 +845,17 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
     // M = 32768: QKV 180.2 -> 153.5 us (256x256 tiles before), out-projection 82.4 -> 66.1, c_proj
     // 199.6 -> 172.3, c_fc with a plain bf16 epilogue 206.1 -> 199.4 (hipBLASLt, plain bf16 out:
     // 146.0 / 64.7 / 139.9 / 148.4)
+    if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
+        // ... and on 256x256 tiles with the 8-phase K loop where that is faster (bit-identical
+        // results): QKV 179.7 -> 155.2 us, c_fc (plain epilogue) 191.4 -> 173.0, c_proj 170.1 ->
+        // 154.5; the out-projection (K = 768, 384 tiles: 1.5 rounds of workgroups) keeps the 128x128
+        // tiles, 60.0 vs 62.3 (profiles/r5_prefill_gemm_8phase.jsonl)
+        // In the bench: prefill 11.2-11.9 -> 10.5-11.2 ms per 1024-query generation
+        // (profiles/r5_prefill_8phase_ab.jsonl)
+        const int kc = K / split;
+        if (M >= 16384 && N % 256 == 0 && kc % 128 == 0 && (EPI != EPI_PARTIAL || kc >= 2048))
+            return launch_gemm8p<EPI>(A, lda, W, ldw, M, N, K, ep, stream);
+    }
     if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF ||
                                     EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
         // (only at the measured size class: 1024-prompt packed prefills; smaller admissions keep the

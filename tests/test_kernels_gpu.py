@@ -92,11 +92,11 @@ def test_gemm_qkv_scatter():
 @pytest.mark.parametrize("epi", ["bf16", "gelu_tanh", "qkv"])
 def test_gemm_256_tiles_large_m(epi, M):
     """Prefill-sized GEMMs: 4096 rows take the 256x256 8-wave tile, the 1024-prompt packed prefill
-    size class (>= 16384 rows) the 128x128 register-staged grouped tiles (asserted by the launch
+    size class (>= 16384 rows) the 256x256 8-phase kernel (both counted as 256x256 launches by the
     census): bias/GELU epilogues and the QKV scatter (packed rows over 4 slots), vs fp32."""
     ops = _ops()
     K = 768
-    tile = (256, 256) if M < 16384 else (128, 128)
+    tile = (256, 256)
     ops.gemm_tile_reset()
     if epi == "qkv":
         H, S = 4, 4
@@ -130,12 +130,12 @@ def test_gemm_256_tiles_large_m(epi, M):
     assert ops.gemm_tile_count(*tile) == 1
 
 
-@pytest.mark.parametrize("tile", [24, 25])
+@pytest.mark.parametrize("tile", [24, 25, 26])
 @pytest.mark.parametrize("epi", ["gelu_tanh", "qkv"])
 def test_gemm_big_modes(tile, epi):
     """The big-GEMM main-loop modes (gemm.hip MODE: REGPF = fragments of a whole K-tile in registers,
     DMA two K-tiles ahead; GROUPED = tiles in groups of 4 row tiles) on 128x128 tiles (ids 24: both,
-    the prefill default; 25: GROUPED only), forced, vs fp32.  M = 4100 leaves a partial last row
+    the prefill default; 25: GROUPED only) and the 8-phase 256x256 kernel (id 26), forced, vs fp32.  M = 4100 leaves a partial last row
     tile and a partial last tile group; the QKV scatter covers the epilogue that the prefill uses."""
     ops = _ops()
     L = ops.lib()
@@ -169,6 +169,53 @@ def test_gemm_big_modes(tile, epi):
             torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
     finally:
         L.dlms_gemm_force_tile(-1)
+
+
+@pytest.mark.parametrize("split,K", [(1, 768), (1, 3072), (2, 3072), (4, 3072)])
+def test_gemm_8phase_partial_slabs(split, K):
+    """The 8-phase kernel's fp32 split-K slabs (out-projection / c_proj of the packed prefill) vs
+    fp32, a partial last row tile included."""
+    ops = _ops()
+    L = ops.lib()
+    M, N = 4100, 768
+    a, w = _bf(M, K, seed=71), _bf(N, K, scale=0.05, seed=72)
+    parts = torch.full((split, M, N), float("nan"), device=DEV)
+    L.dlms_gemm_force_tile(26)
+    try:
+        ops.gemm(a, w, ops.EPI_PARTIAL, out=parts, split_k=split)
+    finally:
+        L.dlms_gemm_force_tile(-1)
+    torch.testing.assert_close(parts.sum(0), a.float() @ w.float().t(), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("N,K,epi", [(2304, 768, "bf16"), (3072, 768, "gelu"), (768, 3072, "partial")])
+def test_gemm_8phase_bit_identical_to_128_tiles_at_prefill_size(N, K, epi):
+    """At the 1024-prompt prefill size the 8-phase kernel sums every output in the same k order as
+    the 128x128 default, so the results are bit-identical -- and identical over repeated launches
+    (a screen for a DMA/read race in its half-tile schedule)."""
+    ops = _ops()
+    L = ops.lib()
+    M = 32768
+    a, w = _bf(M, K, seed=73), _bf(N, K, scale=0.05, seed=74)
+    bias = torch.randn(N, device=DEV) * 0.1
+
+    def run(tile):
+        L.dlms_gemm_force_tile(tile)
+        try:
+            if epi == "partial":
+                out = torch.full((1, M, N), float("nan"), device=DEV)
+                ops.gemm(a, w, ops.EPI_PARTIAL, out=out, split_k=1)
+            else:
+                out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+                ops.gemm(a, w, ops.EPI_GELU_TANH if epi == "gelu" else ops.EPI_BF16, bias=bias, out=out)
+        finally:
+            L.dlms_gemm_force_tile(-1)
+        return out
+
+    ref = run(24)
+    for _ in range(4):
+        got = run(26)
+        assert torch.equal(got, ref)
 
 
 @pytest.mark.parametrize("epi,M,N,K", [("gelu_tanh", 256, 6400, 1600), ("bf16", 300, 4096, 1024),
