@@ -508,9 +508,6 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16_t* __restrict__ 
     const char* Wb = reinterpret_cast<const char*>(W);
     // half-tile slots: buffer b, part q (0 A0, 1 A1, 2 W0, 3 W1)
     auto issue = [&](int b, int q, int kt) {
-#ifdef G8P_DIAG_NODMA
-        if (kt > 1) return;
-#endif
         char* dst = smem + (b * 4 + q) * HALF;
         const int h = q & 1;
         const unsigned kb = (unsigned)kt * 128u;  // 64 bf16 per K-tile
