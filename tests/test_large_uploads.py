@@ -46,9 +46,10 @@ def _wait(pred, timeout=60.0, what=""):
 
 def test_48mib_upload_commits_everywhere_without_leader_change(tmp_path):
     # the three nodes share ONE interpreter (and its GIL) here, and the suite runs under parallel
-    # workers: give elections a 0.4-0.8 s timeout so CPU contention from OTHER tests is not read
-    # as a lost leader (alone, the default 0.15-0.3 s passes too; round 1 lost quorum for seconds)
-    c = Cluster(3, tmp_path, raft_config=RaftConfig(election_timeout=(0.4, 0.8)))
+    # workers: give elections a 1-2 s timeout so CPU contention from OTHER tests is not read as a
+    # lost leader (alone, the default 0.15-0.3 s passes too; round 1 lost quorum for seconds, and
+    # 0.4-0.8 s still saw a term change with 8 xdist workers on 8 CPUs)
+    c = Cluster(3, tmp_path, raft_config=RaftConfig(election_timeout=(1.0, 2.0)))
     try:
         lid = c.wait_leader()
         term0 = c.servers[lid].node.status()["term"]
