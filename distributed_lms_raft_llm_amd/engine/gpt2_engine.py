@@ -498,6 +498,11 @@ class HipGPT2Engine:
             return parts, 1, bias
         if fixed:
             s = max(d for d in range(1, fixed + 1) if (w.shape[1] // 64) % d == 0)
+        elif M >= 16384 and w.shape[1] >= 3072 and w.shape[0] % 256 == 0 and parts.shape[0] >= 2:
+            # packed-prefill c_proj: split 2 -> 768 256x256 tiles on the 8-phase GEMM, three full
+            # rounds of workgroups instead of 1.5 (prefill 10.9-11.8 -> 10.7-11.4 ms per 1024-query
+            # generation, profiles/r5_prefill_cproj_split2_ab.jsonl)
+            s = 2
         elif self.gemm96 and 256 < M <= 512 and w.shape[1] >= 2048 and w.shape[0] % 96 == 0 and \
                 (w.shape[1] // 64) % 4 == 0:
             # c_proj on a 512-row decode half: split 4 -> 64x96 tiles in one round of 256 workgroups
@@ -1025,7 +1030,8 @@ class HipGPT2Engine:
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         f32, bf = torch.float32, torch.bfloat16
         x = ops.embed(tokens_d, pos_d, self.w.wte, self.w.wpe)
-        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl), self.prefill_split or 1)
+        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl), self.prefill_split or 1,
+                     2 if R >= 16384 else 1)  # (c_proj's split 2 at this size: _row_parallel)
         parts = torch.empty(nsplit, R, D, dtype=f32, device=dev)
         h = torch.empty(R, D, dtype=bf, device=dev)
         q = torch.empty(R, Dl, dtype=bf, device=dev)
@@ -1129,7 +1135,7 @@ class HipGPT2Engine:
         last = torch.tensor([sum(lens[: b + 1]) - 1 for b in range(len(prompts))], dtype=torch.int32, device=dev)
         D, Dl, Fl = cfg.n_embd, self.w.d_local, self.w.ffn_local
         x = ops.embed(tokens, pos, self.w.wte, self.w.wpe)
-        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl), self.prefill_split or 1)
+        nsplit = max(self._split(R, D, Fl), self._split(R, D, Dl), self.prefill_split or 1, 2 if R >= 16384 else 1)
         parts = torch.empty(nsplit, R, D, device=dev)
         bf = torch.bfloat16
         h, q, att, ff = (torch.empty(R, n, dtype=bf, device=dev) for n in (D, Dl, Dl, Fl))

@@ -846,11 +846,12 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
         // ... and on 256x256 tiles with the 8-phase K loop where that is faster (bit-identical
         // results): QKV 179.7 -> 155.2 us, c_fc (plain epilogue) 191.4 -> 173.0, c_proj 170.1 ->
         // 154.5; the out-projection (K = 768, 384 tiles: 1.5 rounds of workgroups) keeps the 128x128
-        // tiles, 60.0 vs 62.3 (profiles/r5_prefill_gemm_8phase.jsonl)
+        // tiles, 60.0 vs 62.3 (profiles/r5_prefill_gemm_8phase.jsonl).  The engine splits the prefill
+        // c_proj 2 ways (K slices of 1536: three full rounds of 256 workgroups)
         // In the bench: prefill 11.2-11.9 -> 10.5-11.2 ms per 1024-query generation
         // (profiles/r5_prefill_8phase_ab.jsonl)
         const int kc = K / split;
-        if (M >= 16384 && N % 256 == 0 && kc % 128 == 0 && (EPI != EPI_PARTIAL || kc >= 2048))
+        if (M >= 16384 && N % 256 == 0 && kc % 128 == 0 && (EPI != EPI_PARTIAL || kc >= 1536))
             return launch_gemm8p<EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     }
     if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF ||
