@@ -698,11 +698,17 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16_t* __restrict__ 
         }
 }
 
+// the kernel addresses its operands with 32-bit byte offsets
+static bool gemm8p_fits(int M, int lda, int N, int ldw) {
+    return (size_t)M * lda * 2 < (1ull << 32) && (size_t)N * ldw * 2 < (1ull << 32);
+}
+
 template <int EPI>
 static hipError_t launch_gemm8p(const void* A, int lda, const void* W, int ldw, int M, int N, int K, const GemmEpi& ep,
                                 hipStream_t stream) {
     const int split = EPI == EPI_PARTIAL ? ep.split_k : 1;
-    if (N % 256 != 0 || (K / split) % 128 != 0 || K % split != 0) return hipErrorInvalidValue;
+    if (N % 256 != 0 || (K / split) % 128 != 0 || K % split != 0 || !gemm8p_fits(M, lda, N, ldw))
+        return hipErrorInvalidValue;
     const size_t lds = 8 * 16384;  // >= the 128 x (128 x 4 + 16) B staged fp32 epilogue quadrant
     static bool attr_set = false;
     if (!attr_set) {
@@ -808,7 +814,8 @@ static hipError_t launch_forced(int id, const void* A, int lda, const void* W, i
     // the one-row-tile LM heads, all measured slower, were removed: profiles/r4_prefill_gemm_modes.jsonl,
     // r4_lmhead_tiles_m512.jsonl.)
     if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_QKV || EPI == EPI_PARTIAL)) {
-        if (id == 26 && N % 256 == 0 && (K / (EPI == EPI_PARTIAL ? ep.split_k : 1)) % 128 == 0)
+        if (id == 26 && N % 256 == 0 && (K / (EPI == EPI_PARTIAL ? ep.split_k : 1)) % 128 == 0 &&
+            gemm8p_fits(M, lda, N, ldw))
             return launch_gemm8p<EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     }
     if constexpr (IN == IN_BF16) {
@@ -851,7 +858,8 @@ static hipError_t launch_gemm_epi(const void* A, int lda, const void* W, int ldw
         // In the bench: prefill 11.2-11.9 -> 10.5-11.2 ms per 1024-query generation
         // (profiles/r5_prefill_8phase_ab.jsonl)
         const int kc = K / split;
-        if (M >= 16384 && N % 256 == 0 && kc % 128 == 0 && (EPI != EPI_PARTIAL || kc >= 1536))
+        if (M >= 16384 && N % 256 == 0 && kc % 128 == 0 && (EPI != EPI_PARTIAL || kc >= 1536) &&
+            gemm8p_fits(M, lda, N, ldw))
             return launch_gemm8p<EPI>(A, lda, W, ldw, M, N, K, ep, stream);
     }
     if constexpr (IN == IN_BF16 && (EPI == EPI_BF16 || EPI == EPI_GELU_TANH || EPI == EPI_GELU_ERF ||
