@@ -50,6 +50,13 @@ class TPEngineProxy:
         self._cast(("generate", [list(p) for p in prompts], max_length, float(repetition_penalty)))
         return self.engine.generate(prompts, max_length, repetition_penalty, stats)
 
+    def warm_decode_graphs(self, repetition_penalty: float = 1.2, max_batch: int | None = None):
+        """Every rank captures the same decode graphs: each capture's warm-up step runs the TP
+        collectives, so rank 0 must never capture alone (its peers would sit in
+        ``serve_follower`` waiting for a command while rank 0 waits in the collective)."""
+        self._cast(("warm", float(repetition_penalty), max_batch))
+        return self.engine.warm_decode_graphs(repetition_penalty, max_batch)
+
     def finished_flags(self, B: int):
         return self.engine.finished_flags(B)
 
@@ -98,6 +105,8 @@ def serve_follower(engine, ctrl_group, src: int) -> int:
             engine.decode(cmd[1], cmd[2], cmd[3])
         elif op == "generate":
             engine.generate(cmd[1], cmd[2], cmd[3])
+        elif op == "warm":
+            engine.warm_decode_graphs(cmd[1], cmd[2])
         else:
             raise RuntimeError(f"unknown TP control command {op!r}")
         n += 1

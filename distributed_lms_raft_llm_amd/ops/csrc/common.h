@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #define DLMS_WAVE 64
 
 typedef unsigned short bf16_t;
@@ -282,3 +284,17 @@ struct GemmEpi {
     const float* w_scale;
     int n_slots;  // EPI_QKV: KV-cache slots (the checked build range-checks row_slot against it)
 };
+
+// Opt a kernel into > 64 KiB of dynamic LDS on the CURRENT device, once per (call site, device):
+// the attribute is per device, so a process-wide "done" flag would skip it on a second GPU.  A
+// race between two first launches only sets the attribute twice (idempotent).
+inline hipError_t lds_opt_in(std::atomic<uint64_t>& done_mask, const void* func, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done_mask.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(func, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done_mask.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}

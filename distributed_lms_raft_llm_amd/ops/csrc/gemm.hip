@@ -710,13 +710,9 @@ static hipError_t launch_gemm8p(const void* A, int lda, const void* W, int ldw, 
     if (N % 256 != 0 || (K / split) % 128 != 0 || K % split != 0 || !gemm8p_fits(M, lda, N, ldw))
         return hipErrorInvalidValue;
     const size_t lds = 8 * 16384;  // >= the 128 x (128 x 4 + 16) B staged fp32 epilogue quadrant
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8p_kernel<EPI>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_set{0};  // per device
+    if (hipError_t e = lds_opt_in(attr_set, reinterpret_cast<const void*>(&gemm8p_kernel<EPI>), (int)lds); e != hipSuccess)
+        return e;
     g_tile_count[3][3].fetch_add(1, std::memory_order_relaxed);
     const int tiles = ((M + 255) / 256) * (N / 256) * split;
     hipLaunchKernelGGL(gemm8p_kernel<EPI>, dim3(tiles), dim3(512), lds, stream, reinterpret_cast<const bf16_t*>(A), lda,
@@ -734,13 +730,10 @@ static hipError_t launch_gemm_cfg(const void* A, int lda, const void* W, int ldw
     size_t lds = (size_t)STAGES * (BM + BN) * GEMM_BK * 2;  // 128-B rows for both input types
     const size_t stage_out = (size_t)BM * (BN * (EPI == EPI_PARTIAL ? 4 : 2) + 16);  // LDS-staged epilogue
     if (EPI != EPI_ARGMAX && EPI != EPI_F32 && stage_out > lds) lds = stage_out;
-    static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN, MODE>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_set{0};  // > 64 KiB of dynamic LDS: opted into once per kernel and device
+    if (hipError_t e = lds_opt_in(attr_set, reinterpret_cast<const void*>(&gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN, MODE>),
+                                  (int)lds); e != hipSuccess)
+        return e;
     hipLaunchKernelGGL((gemm_tn_kernel<BM, BN, WM, WN, STAGES, EPI, IN, MODE>), dim3(tiles), dim3(64 * WM * WN), lds, stream, A,
                        lda, W,
                        ldw, M, N, K, ep);

@@ -275,13 +275,10 @@ static hipError_t launch_ps(const void* A, int lda, const void* W, int M, int N,
     const int row_blocks = (M + 16 * MT - 1) / (16 * MT);
     const size_t lds = (size_t)16 * MT * (kc * 2 + PS_PAD) + (size_t)PS_NW * PS_STAGE;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ps_kernel<EPI, MT, NT, KBC, NB>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_set{0};  // per device
+    if (hipError_t e = lds_opt_in(attr_set, reinterpret_cast<const void*>(&gemm_ps_kernel<EPI, MT, NT, KBC, NB>), 160 * 1024);
+        e != hipSuccess)
+        return e;
     hipLaunchKernelGGL((gemm_ps_kernel<EPI, MT, NT, KBC, NB>), dim3(row_blocks * split * col_wgs), dim3(64 * PS_NW), lds, stream,
                        reinterpret_cast<const bf16_t*>(A), lda, reinterpret_cast<const bf16_t*>(W), M, N, K, row_blocks,
                        split, col_wgs, ep);

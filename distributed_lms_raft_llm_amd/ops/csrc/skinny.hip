@@ -265,13 +265,11 @@ static hipError_t launch_skinny(const void* A, int lda, const float* g, const fl
     if (LN) lds = (size_t)16 * MT * (K * 2 + 16);
     const size_t red = (size_t)NW * MT * 64 * 4 * sizeof(float);
     if (NW / CG > 1 && red > lds) lds = red;
-    static bool attr_set = false;
-    if (!attr_set && lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<EPI, LN, MT, NW, CG, KBW>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_set{0};  // per device
+    if (lds > 65536)
+        if (hipError_t e = lds_opt_in(attr_set, reinterpret_cast<const void*>(&skinny_gemm_kernel<EPI, LN, MT, NW, CG, KBW>),
+                                      160 * 1024); e != hipSuccess)
+            return e;
     const int wnt = EPI == SK_ARGMAX ? lm_head_nt() : 0;
     hipLaunchKernelGGL((skinny_gemm_kernel<EPI, LN, MT, NW, CG, KBW>), dim3(N / (16 * CG)), dim3(64 * NW), lds, stream,
                        A, lda, g, b, eps, W, M, N, K, ep, wnt);
@@ -867,13 +865,11 @@ static hipError_t launch_mlp(const void* x_in, int ldx, const float* parts, int 
     } else {
         if (F % (16 * CG)) return hipErrorInvalidValue;
         constexpr int lds = mlp_dyn_lds(RPW, NKB, CG);
-        static bool attr_set = false;
-        if (!attr_set && lds > 65536) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_mlp_kernel<NSPLIT, NV4, RPW, NKB, CG, XFIX>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-            if (e != hipSuccess) return e;
-            attr_set = true;
-        }
+        static std::atomic<uint64_t> attr_set{0};  // per device
+        if (lds > 65536)
+            if (hipError_t e = lds_opt_in(attr_set, reinterpret_cast<const void*>(&skinny_mlp_kernel<NSPLIT, NV4, RPW, NKB, CG, XFIX>),
+                                          lds); e != hipSuccess)
+                return e;
         hipLaunchKernelGGL((skinny_mlp_kernel<NSPLIT, NV4, RPW, NKB, CG, XFIX>), dim3(F / (16 * CG)), dim3(256), lds, stream,
                            x_in, ldx, parts, ldp, sstride, rbias, g, b, eps, Wfc, b_fc, Wp, b_p, r_out, ldr, rcs, xcs, M, base);
         return hipGetLastError();

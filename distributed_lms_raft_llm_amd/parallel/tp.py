@@ -219,6 +219,20 @@ class TorchSlotEngine:
                                    torch.tensor([n - 1], device=self.device), self.caches[s])
                 self._emit(s, h[-1], repetition_penalty)
 
+    @torch.no_grad()
+    def warm_decode_graphs(self, repetition_penalty: float = 1.2, max_batch: int | None = None) -> tuple[int, float]:
+        """The HIP engine's start-up warm-up has no graphs to capture here, but it keeps the same
+        collective contract: one throw-away decode forward on a scratch cache runs the group's
+        all-reduces, so rank 0 calling it alone (not mirrored to the followers) deadlocks exactly
+        like an unmirrored graph capture would (tests/test_tp_serving.py, the torchrun CLI test)."""
+        import time
+
+        t0 = time.perf_counter()
+        eos = self.cfg.eos_token_id
+        self.m.forward(torch.tensor([eos], device=self.device), torch.tensor([0], device=self.device),
+                       self.m.new_cache(1))
+        return 0, time.perf_counter() - t0
+
     def finished_flags(self, B: int) -> list[int]:
         return list(self.fin[:B])
 

@@ -446,7 +446,9 @@ def main(argv=None):
         eng = make_engine(args.model, args.device, args.max_batch, args.max_length, args.weights,
                           weight_dtype=args.weight_dtype)
     args.max_batch = getattr(eng, "max_batch", 0) or args.max_batch or 64
-    if args.warm_batch > 0 and hasattr(eng, "warm_decode_graphs"):  # (single-GPU engines; not a TP proxy)
+    if args.warm_batch > 0 and hasattr(eng, "warm_decode_graphs"):
+        # (a TP proxy mirrors the call to every rank of its group: the captures' warm-up steps run
+        # the group's collectives, engine/tp_serving.py)
         n, secs = eng.warm_decode_graphs(args.repetition_penalty, args.warm_batch)
         log.info("captured %d decode graphs (batch buckets <= %d) in %.1f s", n, args.warm_batch, secs)
     tok = GPT2BPE(args.vocab, args.merges, eos_token_id=eng.cfg.eos_token_id)
