@@ -36,6 +36,18 @@ sys.path.insert(0, ROOT)
 
 BASELINE_TOK_S = 53.7  # reference GPT-2-124M generate on CPU
 METRIC = "tutoring tokens/sec (GPT-2-124M) + p50 query latency at 1/2/4/8 MI355X"
+# other models (BASELINE configs 3-5) report the same measurement under their own name; the
+# published baseline exists for GPT-2-124M in bf16 only, so only that line carries vs_baseline
+MODEL_LABELS = {"gpt2": "GPT-2-124M", "gpt2-medium": "GPT-2-medium (355M)", "gpt2-large": "GPT-2-large (774M)",
+                "gpt2-xl": "GPT-2-XL (1.5B)"}
+
+
+def metric_for(model: str) -> str:
+    return METRIC.replace("GPT-2-124M", MODEL_LABELS.get(model, model))
+
+
+def vs_baseline(model: str, weight_dtype: str, tok_s: float):
+    return round(tok_s / BASELINE_TOK_S, 1) if model == "gpt2" and weight_dtype == "bf16" else None
 
 
 def spawn_ranks(n: int) -> int:
@@ -211,7 +223,7 @@ def main():
         dist.barrier()
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": metric_for(args.model),
             "value": round(tok_s, 1) if tok_s >= 100 else round(tok_s, 4),  # (CPU contract runs: < 1 tok/s)
             "unit": "tokens/s",
             "n_gpus": world if gpu else 0,
@@ -220,7 +232,7 @@ def main():
             "ms_per_step": round(elapsed_max * 1e3 / args.steps, 3),
             "higher_is_better": True,
             "scaling": "weak" if tp == 1 else "strong",
-            "vs_baseline": round(tok_s / BASELINE_TOK_S, 1),
+            "vs_baseline": vs_baseline(args.model, args.weight_dtype, tok_s),
             "dtype": "bf16" if args.weight_dtype == "bf16" else "fp8-w8a8+bf16",
             "data": "synthetic prompts (random token ids), random-init GPT-2-124M weights",
             "p50_query_latency_ms": round(p50, 3),

@@ -87,3 +87,17 @@ def test_bench_reports_latency_points():
     assert p.returncode == 0, p.stderr[-2000:]
     d = _json_lines(p.stdout)[0]
     assert d["p50_query_latency_ms_b1"] > 0 and d["tok_s_b1"] > 0
+
+
+def test_bench_labels_are_model_correct():
+    """Only the BASELINE config (GPT-2-124M, bf16) carries the published metric name's ratio; other
+    models report under their own name with vs_baseline null (BASELINE.md has no number for them)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.metric_for("gpt2") == bench.METRIC
+    assert "GPT-2-XL" in bench.metric_for("gpt2-xl") and "124M" not in bench.metric_for("gpt2-xl")
+    assert "GPT-2-medium" in bench.metric_for("gpt2-medium")
+    assert bench.vs_baseline("gpt2", "bf16", 53.7 * 10) == 10.0
+    assert bench.vs_baseline("gpt2-medium", "bf16", 1e5) is None
+    assert bench.vs_baseline("gpt2", "fp8", 1e5) is None

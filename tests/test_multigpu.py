@@ -25,7 +25,12 @@ def _port():
 
 
 def _init(rank, world, port):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    # (importing the package before the first GPU call sets HSA_ENABLE_IPC_MODE_LEGACY=0 exactly as
+    # the tutor and bench.py get it: distributed_lms_raft_llm_amd/__init__.py)
+    import distributed_lms_raft_llm_amd  # noqa: F401
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    assert os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
     torch.cuda.set_device(rank)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{rank}"))
 
