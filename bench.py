@@ -253,6 +253,8 @@ def main():
             },
         }
         print(json.dumps(line), flush=True)
+    if hasattr(eng, "close"):
+        eng.close()  # graphs, dataflow buffers, xGMI mappings released before interpreter teardown
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -32,7 +32,7 @@ CHECK_SITES = {1: "embed token id", 2: "position id", 3: "decode_update slot_map
                5: "decode_update sequence length", 6: "seen_set row", 7: "QKV scatter slot", 8: "QKV scatter position",
                9: "attention slot", 10: "BERT token id", 11: "seen_set token id"}
 SOURCES = ["api.hip", "gemm.hip", "norm.hip", "attention.hip", "decode.hip", "encoder.hip", "xgmi.hip", "skinny.hip", "gemm_ps.hip",
-           "dataflow.hip"]
+           "dataflow.hip", "mid.hip"]
 ARCH = os.environ.get("DLMS_OFFLOAD_ARCH", "gfx950")
 
 EPI_BF16, EPI_GELU_TANH, EPI_GELU_ERF, EPI_F32, EPI_QKV, EPI_ARGMAX, EPI_PARTIAL = range(7)
@@ -162,6 +162,9 @@ def _bind(L):
         "dlms_ln_fix": [P, I, ctypes.c_longlong, P, P, F, P, I, I, I, P],
         "dlms_fix_copies": [],
         "dlms_skinny_addln_max_rows": [I],
+        "dlms_mid_max_rows": [I],
+        "dlms_mid_ln_gemm": [I, P, I, P, P, F, P, I, I, I, ctypes.POINTER(GemmEpi), I, P],
+        "dlms_mid_proj": [P, I, P, P, P, I, I, I, I, I, P],
         "dlms_gemm_ps": [I, P, I, P, I, I, I, I, I, I, I, ctypes.POINTER(GemmEpi), P],
         "dlms_attention_persist": [P, I, P, P, P, P, P, I, I, I, I, I, F, I, P],
     }
@@ -742,6 +745,63 @@ def unshuffle_weight(ws: torch.Tensor) -> torch.Tensor:
     return ws.reshape(G, KB, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(G * 16, KB * 32)
 
 
+def _skinny_epi(a: torch.Tensor, M: int, N: int, epi: int, bias, out, q_out, k_cache, v_cache, row_slot, row_pos,
+                argmax_out, seen, vocab: int, col_offset: int, penalty: float, name: str = "skinny_gemm"):
+    """GemmEpi of the skinny / mid kernels' column-owning epilogue (skinny_common.h): returns
+    (ep, kernel epilogue id, output tensor)."""
+    ep = GemmEpi()
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() < N:
+            raise ValueError("bias too short")
+        ep.bias = bias.data_ptr()
+    cepi = epi
+    if epi == EPI_F32 and out is not None and out.dtype == torch.int64:
+        cepi = 7  # skinny.hip SK_FIXADD: into copy 0 of the fused MLP's fixed-point residual
+    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_F32, EPI_PARTIAL):
+        want = torch.bfloat16 if epi in (EPI_BF16, EPI_GELU_TANH) else torch.float32
+        if cepi == 7:
+            want = torch.int64
+        if out is None:
+            if epi == EPI_F32:
+                raise ValueError(f"{name} EPI_F32 accumulates into an existing out (the residual)")
+            out = torch.empty(M, N, dtype=want, device=a.device)
+        _req(out, want, "out", 2)
+        if out.shape[0] < M or out.shape[1] < N:
+            raise ValueError("out too small")
+        ep.out, ep.ldo = out.data_ptr(), out.stride(0)
+    elif epi == EPI_QKV:
+        for t, n in ((q_out, "q_out"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+            _req(t, torch.bfloat16, n)
+        _req(row_slot, torch.int32, "row_slot", 1)
+        _req(row_pos, torch.int32, "row_pos", 1)
+        if N % 3 or (N // 3) % 64:
+            raise ValueError("QKV N must be 3 * d_local (64-wide heads)")
+        d_local = N // 3
+        if k_cache.dim() != 4 or k_cache.shape != v_cache.shape or k_cache.shape[1] * 64 != d_local or \
+                k_cache.shape[3] != 64 or not k_cache.is_contiguous() or not v_cache.is_contiguous():
+            raise ValueError(f"cache shape {tuple(k_cache.shape)} incompatible with d_local={d_local}")
+        if q_out.shape[0] < M or q_out.shape[1] < d_local or row_slot.numel() < M or row_pos.numel() < M:
+            raise ValueError("qkv epilogue buffers too small")
+        ep.q_out, ep.ldq = q_out.data_ptr(), q_out.stride(0)
+        ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
+        ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
+        ep.n_heads, ep.t_max, ep.d_local, ep.n_slots = k_cache.shape[1], k_cache.shape[2], d_local, k_cache.shape[0]
+        out = q_out
+    elif epi == EPI_ARGMAX:
+        _req(argmax_out, torch.int64, "argmax_out", 2)
+        _req(seen, torch.int32, "seen", 2)
+        if N % 64 or argmax_out.shape[0] < M or argmax_out.shape[1] < N // 64 or seen.shape[0] < M or \
+                seen.shape[1] * 32 < vocab or col_offset % 64:
+            raise ValueError("argmax epilogue buffers too small / misaligned shard")
+        ep.argmax_out, ep.ldo, ep.seen = argmax_out.data_ptr(), argmax_out.stride(0), seen.data_ptr()
+        ep.seen_words, ep.vocab, ep.col_offset, ep.penalty = seen.stride(0), vocab, col_offset, penalty
+        out = argmax_out
+    else:
+        raise ValueError(f"{name}: unsupported epilogue {epi}")
+    return ep, cepi, out
+
+
 def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=None, out=None,
                 q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None,
                 argmax_out=None, seen=None, vocab: int = 0, col_offset: int = 0, penalty: float = 1.0):
@@ -779,60 +839,71 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
         raise ValueError(f"skinny_gemm: a has K={a.shape[1]}, weight K={K}")
     if M < 1 or M > SKINNY_MAX_M:
         raise ValueError(f"skinny_gemm: 1 <= M <= {SKINNY_MAX_M}")
-    ep = GemmEpi()
-    if bias is not None:
-        _req(bias, torch.float32, "bias", 1)
-        if bias.numel() < N:
-            raise ValueError("bias too short")
-        ep.bias = bias.data_ptr()
-    cepi = epi
-    if epi == EPI_F32 and out is not None and out.dtype == torch.int64:
-        cepi = 7  # skinny.hip SK_FIXADD: into copy 0 of the fused MLP's fixed-point residual
-    if epi in (EPI_BF16, EPI_GELU_TANH, EPI_F32, EPI_PARTIAL):
-        want = torch.bfloat16 if epi in (EPI_BF16, EPI_GELU_TANH) else torch.float32
-        if cepi == 7:
-            want = torch.int64
-        if out is None:
-            if epi == EPI_F32:
-                raise ValueError("skinny_gemm EPI_F32 accumulates into an existing out (the residual)")
-            out = torch.empty(M, N, dtype=want, device=a.device)
-        _req(out, want, "out", 2)
-        if out.shape[0] < M or out.shape[1] < N:
-            raise ValueError("out too small")
-        ep.out, ep.ldo = out.data_ptr(), out.stride(0)
-    elif epi == EPI_QKV:
-        for t, n in ((q_out, "q_out"), (k_cache, "k_cache"), (v_cache, "v_cache")):
-            _req(t, torch.bfloat16, n)
-        _req(row_slot, torch.int32, "row_slot", 1)
-        _req(row_pos, torch.int32, "row_pos", 1)
-        if N % 3 or (N // 3) % 64:
-            raise ValueError("QKV N must be 3 * d_local (64-wide heads)")
-        d_local = N // 3
-        if k_cache.dim() != 4 or k_cache.shape != v_cache.shape or k_cache.shape[1] * 64 != d_local or \
-                k_cache.shape[3] != 64 or not k_cache.is_contiguous() or not v_cache.is_contiguous():
-            raise ValueError(f"cache shape {tuple(k_cache.shape)} incompatible with d_local={d_local}")
-        if q_out.shape[0] < M or q_out.shape[1] < d_local or row_slot.numel() < M or row_pos.numel() < M:
-            raise ValueError("qkv epilogue buffers too small")
-        ep.q_out, ep.ldq = q_out.data_ptr(), q_out.stride(0)
-        ep.k_cache, ep.v_cache = k_cache.data_ptr(), v_cache.data_ptr()
-        ep.row_slot, ep.row_pos = row_slot.data_ptr(), row_pos.data_ptr()
-        ep.n_heads, ep.t_max, ep.d_local, ep.n_slots = k_cache.shape[1], k_cache.shape[2], d_local, k_cache.shape[0]
-        out = q_out
-    elif epi == EPI_ARGMAX:
-        _req(argmax_out, torch.int64, "argmax_out", 2)
-        _req(seen, torch.int32, "seen", 2)
-        if N % 64 or argmax_out.shape[0] < M or argmax_out.shape[1] < N // 64 or seen.shape[0] < M or \
-                seen.shape[1] * 32 < vocab or col_offset % 64:
-            raise ValueError("argmax epilogue buffers too small / misaligned shard")
-        ep.argmax_out, ep.ldo, ep.seen = argmax_out.data_ptr(), argmax_out.stride(0), seen.data_ptr()
-        ep.seen_words, ep.vocab, ep.col_offset, ep.penalty = seen.stride(0), vocab, col_offset, penalty
-        out = argmax_out
-    else:
-        raise ValueError(f"skinny_gemm: unsupported epilogue {epi}")
+    ep, cepi, out = _skinny_epi(a, M, N, epi, bias, out, q_out, k_cache, v_cache, row_slot, row_pos, argmax_out, seen,
+                                vocab, col_offset, penalty)
     lg, lb, le = (ln[0], ln[1], float(ln[2])) if ln is not None else (None, None, 0.0)
     _check(lib().dlms_skinny_gemm(cepi, _p(a), a.stride(0), _p(lg), _p(lb), le, _p(w_sh), M, N, K, ctypes.byref(ep),
                                   _stream()), "dlms_skinny_gemm")
     return out
+
+
+def mid_max_rows(K: int) -> int:
+    """Largest M the mid-batch fused LayerNorm + GEMM (``mid_ln_gemm``) takes at width K (0: none)."""
+    return int(lib().dlms_mid_max_rows(int(K)))
+
+
+def mid_ln_gemm(x: torch.Tensor, w_sh: torch.Tensor, epi: int, gamma, beta, eps: float, *, bias=None, out=None,
+                q_out=None, k_cache=None, v_cache=None, row_slot=None, row_pos=None, geo: int = 0):
+    """Mid-batch decode (9-64 rows) LN1 -> QKV / LN2 -> c_fc in one kernel (mid.hip):
+    ``out = epi(bf16(LN(x)) @ W.T + bias)`` for the f32 residual rows ``x`` [M, K] (complete: the
+    mid path's projections update the residual in place) against a ``shuffle_weight`` weight.
+    epi: EPI_QKV (q out + K/V cache scatter), EPI_GELU_TANH or EPI_BF16 (bf16 ``out``).
+    ``geo``: 0 = default geometry, 1..5 tuning overrides (waves / column groups per workgroup)."""
+    _req(x, torch.float32, "x", 2)
+    _req(w_sh, torch.bfloat16, "w_sh", 4)
+    G, KB = w_sh.shape[0], w_sh.shape[1]
+    if w_sh.shape[2] != 64 or w_sh.shape[3] != 8 or not w_sh.is_contiguous():
+        raise ValueError("mid_ln_gemm: w_sh must be a contiguous shuffle_weight() tensor")
+    N, K = G * 16, KB * 32
+    M = x.shape[0]
+    if x.shape[1] != K or M < 1 or M > mid_max_rows(K) or x.stride(0) % 4 or x.data_ptr() % 16:
+        raise ValueError(f"mid_ln_gemm: x {tuple(x.shape)} vs K={K} (max rows {mid_max_rows(K)}, 16-B aligned rows)")
+    for t, n in ((gamma, "gamma"), (beta, "beta")):
+        _req(t, torch.float32, n, 1)
+        if t.numel() != K:
+            raise ValueError(f"mid_ln_gemm: {n} size")
+    if epi not in (EPI_QKV, EPI_GELU_TANH, EPI_BF16):
+        raise ValueError("mid_ln_gemm: QKV / GELU / bf16 epilogues")
+    ep, cepi, out = _skinny_epi(x, M, N, epi, bias, out, q_out, k_cache, v_cache, row_slot, row_pos, None, None, 0, 0,
+                                1.0, name="mid_ln_gemm")
+    _check(lib().dlms_mid_ln_gemm(cepi, _p(x), x.stride(0), _p(gamma), _p(beta), float(eps), _p(w_sh), M, N, K,
+                                  ctypes.byref(ep), int(geo), _stream()), "dlms_mid_ln_gemm")
+    return out
+
+
+def mid_proj(a: torch.Tensor, w_sh: torch.Tensor, x: torch.Tensor, *, bias=None, geo: int = 0) -> torch.Tensor:
+    """Mid-batch (<= 64 rows) in-place row-parallel projection (mid.hip): ``x += a @ W.T + bias``
+    with column-owning workgroups (out-projection, c_proj).  a: bf16 [M, K]; x: f32 [M, N];
+    ``w_sh``: ``shuffle_weight`` layout.  K/32 must split evenly over the geometry's waves."""
+    _req(a, torch.bfloat16, "a", 2)
+    _req(x, torch.float32, "x", 2)
+    _req(w_sh, torch.bfloat16, "w_sh", 4)
+    G, KB = w_sh.shape[0], w_sh.shape[1]
+    if w_sh.shape[2] != 64 or w_sh.shape[3] != 8 or not w_sh.is_contiguous():
+        raise ValueError("mid_proj: w_sh must be a contiguous shuffle_weight() tensor")
+    N, K = G * 16, KB * 32
+    M = a.shape[0]
+    if a.shape[1] != K or x.shape[0] != M or x.shape[1] != N or not 1 <= M <= 64:
+        raise ValueError(f"mid_proj: a {tuple(a.shape)}, x {tuple(x.shape)} vs W [{N}, {K}] (1 <= M <= 64)")
+    if a.stride(0) % 8 or a.data_ptr() % 16:
+        raise ValueError("mid_proj: bf16 A rows must be 16-byte aligned")
+    if bias is not None:
+        _req(bias, torch.float32, "bias", 1)
+        if bias.numel() < N:
+            raise ValueError("mid_proj: bias too short")
+    _check(lib().dlms_mid_proj(_p(a), a.stride(0), _p(w_sh), _p(bias), _p(x), x.stride(0), M, N, K, int(geo),
+                               _stream()), "dlms_mid_proj")
+    return x
 
 
 def skinny_addln_max_rows(K: int) -> int:

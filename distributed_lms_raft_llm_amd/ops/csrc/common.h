@@ -19,15 +19,16 @@ __device__ __forceinline__ float bf16_to_f32(bf16_t v) {
 
 // Round-to-nearest-even f32 -> bf16 (inputs are finite activations; NaN handling not needed
 // on this path, but keep NaN a NaN anyway by forcing the quiet bit).
-__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
-    unsigned int u = __float_as_uint(f);
-    if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
-}
+// f32 -> bf16, round to nearest even (NaN stays NaN): gfx950's v_cvt_pk_bf16_f32, one VALU op for
+// two values.  (The integer rounding sequence it replaces compiled to ~18 instructions with an
+// exec-mask branch per element: 1-1.5 us of every LayerNorm prologue at 32 rows.)  Same results
+// for every finite input, f32 denormals included (HIP keeps them unflushed).
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 __device__ __forceinline__ unsigned int pack_bf16x2(float lo, float hi) {
-    return (unsigned int)f32_to_bf16(lo) | ((unsigned int)f32_to_bf16(hi) << 16);
+    typedef __bf16 bf16x2_hw_t __attribute__((ext_vector_type(2)));
+    const bf16x2_hw_t v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(unsigned int, v);
 }
 
 // unpack 8 bf16 held in a uint4 into floats

@@ -62,6 +62,48 @@ __device__ __forceinline__ void wait_vmcnt() {
 //          workgroups an XCD runs at once share 4 A panels and 8 W panels through its L2 (the
 //          column-major order gave every one of them its own A panel: 32 panels from beyond L2)
 #define GROUP_M 4
+// Write-out of an LDS-staged bf16 QKV tile (rows [r0, r0 + CHUNKS / CPR), columns from c0, CPR
+// 16-B chunks per row): q columns go to q_out, K/V columns to each row's cache slot / position.
+// Every chunk's slot / position index is loaded before the first store -- interleaved with the
+// stores they cost one dependent L2 round trip per chunk (3-8 per thread per tile).
+template <int CHUNKS, int NT, int CPR>
+__device__ __forceinline__ void qkv_staged_store(const char* smem, int srow, int tid, int r0, int c0, int M,
+                                                 const GemmEpi& ep) {
+    constexpr int ITER = (CHUNKS + NT - 1) / NT;
+    int sl[ITER], ps[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        int c = tid + it * NT;
+        c = c < CHUNKS ? c : CHUNKS - 1;
+        int row = r0 + c / CPR;
+        row = row < M ? row : M - 1;
+        sl[it] = ep.row_slot[row];
+        ps[it] = ep.row_pos[row];
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+        const int c = tid + it * NT;
+        if (c >= CHUNKS) break;
+        const int lr = c / CPR, ch = c - lr * CPR;
+        const int row = r0 + lr;
+        if (row >= M) continue;
+        const uint4 val = *reinterpret_cast<const uint4*>(smem + lr * srow + ch * 16);
+        const int col = c0 + ch * 8;
+        const int part = col / ep.d_local;
+        const int within = col - part * ep.d_local;
+        bf16_t* dst;
+        if (part == 0) {
+            dst = ep.q_out + (size_t)row * ep.ldq + within;
+        } else {
+            const int head = within >> 6, dim = within & 63;
+            const size_t slot = dlms_idx(sl[it], ep.n_slots, CHK_QKV_SLOT);
+            const size_t pos = dlms_idx(ps[it], ep.t_max, CHK_QKV_POS);
+            dst = (part == 1 ? ep.k_cache : ep.v_cache) + ((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim;
+        }
+        *reinterpret_cast<uint4*>(dst) = val;
+    }
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, int EPI, int IN, int MODE = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __restrict__ A, int lda,
                                                       const void* __restrict__ W, int ldw, int M, int N,
@@ -371,6 +413,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
                 }
         }
         __syncthreads();
+        if constexpr (EPI == EPI_QKV) {
+            qkv_staged_store<BM * CPR, NT, CPR>(smem, SROW, tid, m0, n0, M, ep);
+            return;
+        }
         for (int c = tid; c < BM * CPR; c += NT) {
             const int lr = c / CPR, ch = c - lr * CPR;
             const int row = m0 + lr;
@@ -380,19 +426,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(const void* __res
             if constexpr (EPI == EPI_PARTIAL) {
                 *reinterpret_cast<uint4*>(reinterpret_cast<float*>(ep.out) + (size_t)split * ep.split_stride +
                                           (size_t)row * ep.ldo + col) = val;
-            } else if constexpr (EPI == EPI_QKV) {
-                const int part = col / ep.d_local;
-                const int within = col - part * ep.d_local;
-                bf16_t* dst;
-                if (part == 0) {
-                    dst = ep.q_out + (size_t)row * ep.ldq + within;
-                } else {
-                    const int head = within >> 6, dim = within & 63;
-                    const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
-                    const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
-                    dst = (part == 1 ? ep.k_cache : ep.v_cache) + ((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim;
-                }
-                *reinterpret_cast<uint4*>(dst) = val;
             } else {
                 *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(ep.out) + (size_t)row * ep.ldo + col) = val;
             }
@@ -668,6 +701,11 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16_t* __restrict__ 
                     }
             }
             __syncthreads();
+            if constexpr (EPI == EPI_QKV) {
+                qkv_staged_store<128 * CPR, 512, CPR>(smem, SROW, tid, m0 + mq * 128, n0 + nq * 128, M, ep);
+                __syncthreads();
+                continue;
+            }
             for (int c = tid; c < 128 * CPR; c += 512) {
                 const int lr = c / CPR, ch = c - lr * CPR;
                 const int row = m0 + mq * 128 + lr;
@@ -677,19 +715,6 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(const bf16_t* __restrict__ 
                 if constexpr (EPI == EPI_PARTIAL) {
                     *reinterpret_cast<uint4*>(reinterpret_cast<float*>(ep.out) + (size_t)split * ep.split_stride +
                                               (size_t)row * ep.ldo + col) = val;
-                } else if constexpr (EPI == EPI_QKV) {
-                    const int part = col / ep.d_local;
-                    const int within = col - part * ep.d_local;
-                    bf16_t* dst;
-                    if (part == 0) {
-                        dst = ep.q_out + (size_t)row * ep.ldq + within;
-                    } else {
-                        const int head = within >> 6, dim = within & 63;
-                        const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
-                        const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
-                        dst = (part == 1 ? ep.k_cache : ep.v_cache) + ((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim;
-                    }
-                    *reinterpret_cast<uint4*>(dst) = val;
                 } else {
                     *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(ep.out) + (size_t)row * ep.ldo + col) = val;
                 }

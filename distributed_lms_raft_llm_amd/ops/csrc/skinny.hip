@@ -20,12 +20,10 @@
 // EPI_F32 (x += acc + bias, in place) / EPI_PARTIAL (TP: raw partial for the all-reduce) /
 // EPI_ARGMAX (repetition penalty + per-row argmax key per 64 columns, the LM-head layout of gemm.hip).
 #include "common.h"
+#include "skinny_common.h"
 #include <type_traits>
 #include <stdlib.h>
 
-// SK_FIXADD: like SK_F32 (x += acc + bias, column-owning, in place) into copy 0 of the int64
-// fixed-point residual the fused MLP accumulates (see DLMS_FIX_SCALE below)
-enum { SK_BF16 = 0, SK_GELU_TANH = 1, SK_F32 = 3, SK_QKV = 4, SK_ARGMAX = 5, SK_PARTIAL = 6, SK_FIXADD = 7 };
 
 #define SK_MAX_LN_V4 8  // LN prologue: K <= 64 lanes * 4 * 8 = 2048
 
@@ -39,10 +37,6 @@ __device__ __forceinline__ bf16x8_t load_wfrag(const bf16x8_t* p) { return *p; }
 // an LRU cache of about that size would otherwise miss on every layer).
 static int lm_head_nt() { return 1; }
 
-// A fragment of rows [16 mt, 16 mt + 16) at k-block kb from the LDS LayerNorm image
-__device__ __forceinline__ bf16x8_t lds_a_frag(const char* img, int row_bytes, int row, int kb, int g) {
-    return *reinterpret_cast<const bf16x8_t*>(img + row * row_bytes + (kb * 32 + g * 8) * 2);
-}
 
 // LayerNorm of rows [0, M) of x (f32, ldx) into an LDS bf16 image of 16*MT rows (rows >= M zero).
 // Wave w normalises rows w, w + NW, ...; two-pass statistics in fp32 like norm.hip.
@@ -93,45 +87,6 @@ __device__ __forceinline__ void ln_prologue(const float* __restrict__ x, int ldx
             }
         }
     }
-}
-
-// Column-owning epilogue of one wave: accumulator element r of row tile t is (row 16t + 4g + r, col).
-template <int EPI, int MT>
-__device__ __forceinline__ void skinny_store(const f32x4_t* acc, int M, int col, int g, const GemmEpi& ep) {
-    const float bv = (EPI != SK_PARTIAL && ep.bias) ? ep.bias[col] : 0.f;
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 16 * t + g * 4 + r;
-            if (row >= M) continue;
-            float v = acc[t][r] + bv;
-            if constexpr (EPI == SK_BF16) {
-                reinterpret_cast<bf16_t*>(ep.out)[(size_t)row * ep.ldo + col] = f32_to_bf16(v);
-            } else if constexpr (EPI == SK_GELU_TANH) {
-                reinterpret_cast<bf16_t*>(ep.out)[(size_t)row * ep.ldo + col] = f32_to_bf16(gelu_tanh(v));
-            } else if constexpr (EPI == SK_F32) {
-                float* o = reinterpret_cast<float*>(ep.out) + (size_t)row * ep.ldo + col;
-                *o = *o + v;  // residual stream, updated in place (x is not an operand of this GEMM)
-            } else if constexpr (EPI == SK_FIXADD) {
-                long long* o = reinterpret_cast<long long*>(ep.out) + (size_t)row * ep.ldo + col;
-                *o = *o + __float2ll_rn(v * 4294967296.0f);  // DLMS_FIX_SCALE (defined further down)
-            } else if constexpr (EPI == SK_PARTIAL) {
-                reinterpret_cast<float*>(ep.out)[(size_t)row * ep.ldo + col] = acc[t][r];
-            } else if constexpr (EPI == SK_QKV) {
-                const int part = col / ep.d_local;
-                const int within = col - part * ep.d_local;
-                const bf16_t hv = f32_to_bf16(v);
-                if (part == 0) {
-                    ep.q_out[(size_t)row * ep.ldq + within] = hv;
-                } else {
-                    const int head = within >> 6, dim = within & 63;
-                    const size_t slot = dlms_idx(ep.row_slot[row], ep.n_slots, CHK_QKV_SLOT);
-                    const size_t pos = dlms_idx(ep.row_pos[row], ep.t_max, CHK_QKV_POS);
-                    (part == 1 ? ep.k_cache : ep.v_cache)[((slot * ep.n_heads + head) * ep.t_max + pos) * 64 + dim] = hv;
-                }
-            }
-        }
 }
 
 // grid.x = column-group blocks of CG groups (16 columns each); block = 64*NW threads.

@@ -439,6 +439,8 @@ def main(argv=None):
         if rank != src:
             n = serve_follower(eng, ctrl, src)
             log.info("TP follower rank %d done after %d commands", rank, n)
+            if hasattr(eng, "close"):
+                eng.close()
             return
         proxy = eng = TPEngineProxy(eng, ctrl, src)
         args.port += dp_idx
@@ -482,7 +484,10 @@ def main(argv=None):
     done.wait()
     srv.stop()
     if proxy is not None:
-        proxy.close()
+        proxy.close()  # releases the followers, which close their engines (below, same order)
+        eng = proxy.engine
+    if hasattr(eng, "close"):
+        eng.close()  # (TP: every rank of the group, the xGMI teardown is collective)
     if fatal:  # exit, never re-exec: a supervisor starts a fresh process on a clean device state
         log.error("exiting with status %d after a fatal serving error", EXIT_FATAL)
         os._exit(EXIT_FATAL)

@@ -66,15 +66,32 @@ def main():
                 h = torch.randn(M, K, device=dev).to(torch.bfloat16)
                 epi = ops.EPI_GELU_TANH if op == "fc" else ops.EPI_BF16
                 out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-                res["skinny_ln"] = graph_time(lambda i: ops.skinny_gemm(x, wsh[i % copies], epi, ln=(g, b, 1e-5),
+                if M <= ops.SKINNY_MAX_M:
+                    res["skinny_ln"] = graph_time(lambda i: ops.skinny_gemm(x, wsh[i % copies], epi, ln=(g, b, 1e-5),
                                                                          bias=bias, out=out))
                 res["tiled+ln"] = graph_time(lambda i: (ops.layernorm(x, g, b, 1e-5, out_bf16=h),
                                                         ops.gemm(h, ws[i % copies], epi, bias=bias, out=out)))
+                if M > 1 and M <= ops.mid_max_rows(K):  # mid.hip: the 9-64-row fused LN + GEMM, per geometry
+                    for geo in (1, 2, 3, 4, 5, 6, 7):
+                        try:
+                            res[f"mid_ln_g{geo}"] = graph_time(
+                                lambda i, geo=geo: ops.mid_ln_gemm(x, wsh[i % copies], epi, g, b, 1e-5, bias=bias,
+                                                                   out=out, geo=geo))
+                        except RuntimeError:
+                            pass
             elif op in ("oproj", "proj"):
                 a = torch.randn(M, K, device=dev).to(torch.bfloat16)
                 x = torch.randn(M, N, device=dev)
-                res["skinny_resid"] = graph_time(lambda i: ops.skinny_gemm(a, wsh[i % copies], ops.EPI_F32, bias=bias,
+                if M <= ops.SKINNY_MAX_M:
+                    res["skinny_resid"] = graph_time(lambda i: ops.skinny_gemm(a, wsh[i % copies], ops.EPI_F32, bias=bias,
                                                                             out=x))
+                if M > 1:  # mid.hip's in-place projection, per geometry
+                    for geo in (1, 2, 3, 4, 5, 6):
+                        try:
+                            res[f"mid_proj_g{geo}"] = graph_time(
+                                lambda i, geo=geo: ops.mid_proj(a, wsh[i % copies], x, bias=bias, geo=geo))
+                        except RuntimeError:
+                            pass
                 parts = torch.empty(8, M, N, device=dev)
                 res["tiled_split4"] = graph_time(lambda i: ops.gemm(a, ws[i % copies], ops.EPI_PARTIAL, out=parts,
                                                                     split_k=4))
@@ -82,7 +99,8 @@ def main():
                 h = torch.randn(M, K, device=dev).to(torch.bfloat16)
                 keys = torch.zeros(M, N // 64, dtype=torch.int64, device=dev)
                 seen = torch.zeros(M, N // 32, dtype=torch.int32, device=dev)
-                res["skinny_argmax"] = graph_time(lambda i: ops.skinny_gemm(h, wsh[i % copies], ops.EPI_ARGMAX,
+                if M <= ops.SKINNY_MAX_M:
+                    res["skinny_argmax"] = graph_time(lambda i: ops.skinny_gemm(h, wsh[i % copies], ops.EPI_ARGMAX,
                                                                              argmax_out=keys, seen=seen, vocab=50257,
                                                                              penalty=1.2))
                 res["tiled_argmax"] = graph_time(lambda i: ops.gemm(h, ws[i % copies], ops.EPI_ARGMAX, argmax_out=keys,
