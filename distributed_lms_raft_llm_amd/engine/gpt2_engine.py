@@ -261,6 +261,12 @@ class HipGPT2Engine:
         # copies -- at <= 8 rows the decode is bound by launch and dependency latency, not weight bytes;
         # W8A8 serves the prefill and the larger batches, where the weight stream matters)
         self.small_max = ops.skinny_addln_max_rows(cfg.n_embd) if latency_path else 0
+        # the mid path (below) serves 3+ rows faster than the fused add+LN latency path: batch 4
+        # 35.9 vs 37.7 ms per query, batch 8 37.3 vs 41.0; batch 2 stays here (34.1 vs 35.2, the fused
+        # MLP) -- profiles/r6_mid_sweep.jsonl.  DLMS_SMALL_MAX_ROWS moves the boundary.
+        if latency_path and self.tp_size == 1 and ops.mid_max_rows(cfg.n_embd) and \
+                os.environ.get("DLMS_MID_PATH", "1") != "0":
+            self.small_max = min(self.small_max, int(os.environ.get("DLMS_SMALL_MAX_ROWS", "2")))
         inplace_ok = self.tp_size == 1 and os.environ.get("DLMS_SMALL_INPLACE", "1") != "0"
         if self.tp_size == 1 and not inplace_ok and \
                 any((k // 64) % self.SMALL_SPLIT for k in (self.w.d_local, self.w.ffn_local)):
@@ -788,14 +794,13 @@ class HipGPT2Engine:
     def _mid_ok(self, B: int) -> bool:
         return self.small_max < B <= self.mid_max
 
-    def _decode_step_mid(self, B: int, penalty: float):
-        """Mid-batch decode step (``mid_max`` in __init__): per layer [LN1 + QKV + K/V scatter] ->
-        split-K attention -> out-projection, x += in place -> [LN2 + c_fc + GELU] -> c_proj, x += in
-        place; then ln_f, the LM head with the fused penalty / argmax, and the bookkeeping."""
+    def _mid_layers(self, lo: int, hi: int):
+        """The mid path's 12 layers on rows [lo, hi): per layer [LN1 + QKV + K/V scatter] -> split-K
+        attention -> out-projection, x += in place -> [LN2 + c_fc + GELU] -> c_proj, x += in place."""
         eps = self.cfg.layer_norm_epsilon
-        x = self.x[:B]
-        r = self._rows(self.x, self.parts, self.h, self.q, self.att, self.ff, self.slots[:B], self.cur_pos[:B],
-                       self.cur_kvlen[:B], B)
+        x = self.x[lo:hi]
+        r = self._rows(self.x[lo:hi], self.parts, self.h[lo:hi], self.q[lo:hi], self.att[lo:hi], self.ff[lo:hi],
+                       self.slots[lo:hi], self.cur_pos[lo:hi], self.cur_kvlen[lo:hi], hi - lo)
         for li, lw in enumerate(self.w.layers):
             ops.mid_ln_gemm(x, lw.w_qkv_sh, ops.EPI_QKV, lw.ln1_g, lw.ln1_b, eps, bias=lw.b_qkv, q_out=r.q,
                             k_cache=self.kv[li, 0], v_cache=self.kv[li, 1], row_slot=r.row_slot, row_pos=r.row_pos)
@@ -803,8 +808,17 @@ class HipGPT2Engine:
             ops.mid_proj(r.att, lw.w_o_sh, x, bias=lw.b_o)
             ops.mid_ln_gemm(x, lw.w_fc_sh, ops.EPI_GELU_TANH, lw.ln2_g, lw.ln2_b, eps, bias=lw.b_fc, out=r.ff)
             ops.mid_proj(r.ff, lw.w_p_sh, x, bias=lw.b_p)
-        ops.layernorm(x, self.w.lnf_g, self.w.lnf_b, eps, out_bf16=r.h)
-        self._lm_head_and_update(r.h, B, penalty)
+
+    def _decode_step_mid(self, B: int, penalty: float):
+        """Mid-batch decode step (``mid_max`` in __init__): the layers (``_mid_layers``), then ln_f,
+        the LM head with the fused penalty / argmax, and the bookkeeping.  (Measured and removed: the
+        two row halves' layers on two HIP streams joined for one LM head -- batch 32 50.4 vs 44.1 ms,
+        batch 64 53.8 vs 51.9, profiles/r6_mid_sweep.jsonl: the row-blocked kernels already fill the
+        chip.)"""
+        eps = self.cfg.layer_norm_epsilon
+        self._mid_layers(0, B)
+        ops.layernorm(self.x[:B], self.w.lnf_g, self.w.lnf_b, eps, out_bf16=self.h[:B])
+        self._lm_head_and_update(self.h[:B], B, penalty)
 
     def _decode_step_small(self, B: int, penalty: float, lo: int = 0):
         """Latency-shaped decode step for B <= ``small_max`` rows: per layer

@@ -64,8 +64,8 @@ def _assert_teacher_forced(model, outs, prompts, eps=0.05, min_decisive=0.7):
 @pytest.mark.parametrize("name,batch", [("gpt2-tiny", 3), ("gpt2", 1), ("gpt2", 3), ("gpt2", 8), ("gpt2", 24),
                                         ("gpt2-medium", 1), ("gpt2-medium", 2), ("gpt2-xl", 2)])
 def test_generate_matches_reference_tokens(name, batch):
-    """bf16 engine vs fp32 oracle, margin-aware and exact: batch 3/8 run the latency path
-    (fused add+LN skinny GEMMs, split-K attention), 24 the tiled path."""
+    """bf16 engine vs fp32 oracle, margin-aware and exact: batch 1 runs the dataflow decode, 2 the
+    latency path, 3/8/24 the mid path (tests/test_mid_gpu.py covers it in depth)."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
     from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference
 
@@ -79,12 +79,14 @@ def test_generate_matches_reference_tokens(name, batch):
     _assert_teacher_forced(GPT2Reference(cfg, w, device="cuda"), got, prompts)
 
 
-def test_latency_path_matches_tiled_path():
-    """The latency-shaped decode step (B <= 8) and the tiled step produce the same greedy tokens
-    under the margin rule (both checked against the fp32 oracle), and the path is actually taken."""
+def test_latency_path_matches_tiled_path(monkeypatch):
+    """The latency-shaped decode step (B <= 8; by default it serves B <= 2 and the mid path 3+,
+    DLMS_SMALL_MAX_ROWS widens it back) and the tiled step produce the same greedy tokens under the
+    margin rule (both checked against the fp32 oracle), and the path is actually taken."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
     from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference
 
+    monkeypatch.setenv("DLMS_SMALL_MAX_ROWS", "8")
     cfg, w = _setup("gpt2")
     prompts = _prompts(cfg, [7, 19, 3, 32], seed=9)
     fast = HipGPT2Engine(cfg, w, max_batch=4, max_length=64)
@@ -128,6 +130,7 @@ def test_fused_mlp_small_batch(batch, rows, monkeypatch):
     from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference
 
     monkeypatch.setenv("DLMS_FUSED_MLP_ROWS", rows)
+    monkeypatch.setenv("DLMS_SMALL_MAX_ROWS", "8")  # (3+ rows default to the mid path)
     cfg, w = _setup("gpt2")
     prompts = _prompts(cfg, [13, 4, 27][:batch], seed=23)
     eng = HipGPT2Engine(cfg, w, max_batch=8, max_length=64)
@@ -230,7 +233,7 @@ def test_warm_decode_graphs_covers_first_use():
 
 @pytest.mark.parametrize("batch", [1, 2, 5, 24])
 def test_multi_step_graph_small_paths(batch, monkeypatch):
-    """Latency path (fused MLP at 1-2 rows, 4-kernel step at 5) and the tiled step (24 rows) with
+    """Latency path (fused MLP at 1-2 rows) and the mid path (5, 24 rows) with
     4 steps per graph replay: the same tokens as one step per replay."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
 
