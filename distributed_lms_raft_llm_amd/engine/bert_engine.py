@@ -19,11 +19,16 @@ from ..models.config import BertConfig
 
 
 class HipBertEncoder:
-    def __init__(self, cfg: BertConfig, weights: dict[str, torch.Tensor], device=None, use_graph: bool | None = None):
+    def __init__(self, cfg: BertConfig, weights: dict[str, torch.Tensor], device=None, use_graph: bool | None = None,
+                 graph_max_rows: int | None = None, graph_max_seqs: int | None = None):
+        """``graph_max_rows`` / ``graph_max_seqs``: the largest pass replayed from a hipGraph (bigger
+        ones run eagerly); the tutor-served gate uses 8192 / 256 for its cross-node passes."""
         if not torch.cuda.is_available():
             raise RuntimeError("HipBertEncoder needs a GPU")
         ops.lib()
         self.cfg = cfg
+        self.graph_max_rows = int(graph_max_rows or self.GRAPH_MAX_ROWS)
+        self.graph_max_seqs = int(graph_max_seqs or self.GRAPH_MAX_SEQS)
         if use_graph is None:
             use_graph = os.environ.get("DLMS_GATE_GRAPH", "1") != "0"
         self.use_graph = use_graph
@@ -88,8 +93,8 @@ class HipBertEncoder:
             Rb = max(64, 1 << (R - 1).bit_length())
             n_dummy = -(-(Rb - R) // cfg.max_position)
             # one bucket dimension only (rows): every pass has GRAPH_MAX_SEQS sequence slots
-            if Rb <= self.GRAPH_MAX_ROWS and n + n_dummy <= self.GRAPH_MAX_SEQS:
-                return self._embed_graphed(batch, lens_np, Rb, self.GRAPH_MAX_SEQS)
+            if Rb <= self.graph_max_rows and n + n_dummy <= self.graph_max_seqs:
+                return self._embed_graphed(batch, lens_np, Rb, self.graph_max_seqs)
         return self._embed_eager(batch, lens_np)
 
     def warm_graphs(self, max_rows: int | None = None) -> int:
@@ -98,7 +103,7 @@ class HipBertEncoder:
         if not self.use_graph:
             return 0
         Rb = 64
-        while Rb <= min(max_rows or self.GRAPH_MAX_ROWS, self.GRAPH_MAX_ROWS):
+        while Rb <= min(max_rows or self.graph_max_rows, self.graph_max_rows):
             L = self.cfg.max_position
             rows = Rb // 2 + 1  # lands in bucket Rb
             self.embed([[101] * min(L, rows - i * L) for i in range(-(-rows // L))])
@@ -124,7 +129,7 @@ class HipBertEncoder:
         cfg, dev = self.cfg, self.device
         H, nh, S = cfg.hidden, cfg.n_head, cfg.max_position
         if self._gbuf is None:  # activations shared by every bucket, sized for the largest
-            Rm, nm = self.GRAPH_MAX_ROWS, self.GRAPH_MAX_SEQS
+            Rm, nm = self.graph_max_rows, self.graph_max_seqs
             bf = torch.bfloat16
             self._gbuf = dict(q=torch.empty(Rm, H, dtype=bf, device=dev), att=torch.empty(Rm, H, dtype=bf, device=dev),
                               ff=torch.empty(Rm, cfg.intermediate, dtype=bf, device=dev),
@@ -216,7 +221,7 @@ class HipBertEncoder:
             self._run_layers(*args)
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             self._run_layers(*args)
         return graph
 

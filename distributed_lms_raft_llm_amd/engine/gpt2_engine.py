@@ -992,7 +992,7 @@ class HipGPT2Engine:
             # (one graph per row part replayed on its own stream measured identical to this one
             # forked graph: 668.07 vs 668.08 k tok/s, profiles/r2_sweep_split_graphs.jsonl)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._decode_step(B, penalty, nsteps)
             self._restore_state(B, saved)
             self._graphs[key] = g
@@ -1159,7 +1159,7 @@ class HipGPT2Engine:
             args = (d[:R], d[R:2 * R], d[2 * R:3 * R], d[o:o + n], d[o + n:o + 2 * n], d[o + 2 * n:o + 3 * n], tiles,
                     penalty)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._prefill_core(*args)
             st["graph"], st["penalty"] = g, penalty
         st["graph"].replay()

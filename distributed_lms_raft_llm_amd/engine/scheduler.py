@@ -111,8 +111,24 @@ class ContinuousBatcher:
         self._error: BaseException | None = None
         self.steps = 0
         self.completed = 0
+        # side work run on this thread between decode chunks (gate/service.py GateWorker: the relevance
+        # gate's encoder passes go on the decode stream right behind a chunk, never interleaved
+        # kernel by kernel with it): work(idle) is called once per loop iteration, pending() says
+        # whether it has anything queued or in flight (so an idle batcher does not sleep on it)
+        self._side_work = None
+        self._side_pending = None
         self._thread = threading.Thread(target=self._run, name=f"{name}-batcher", daemon=True)
         self._thread.start()
+
+    def attach_side_work(self, work, pending):
+        with self._cv:
+            self._side_work, self._side_pending = work, pending
+            self._cv.notify()
+
+    def kick(self):
+        """Wake the scheduler thread (new side work arrived)."""
+        with self._cv:
+            self._cv.notify()
 
     # ------------------------------------------------------------------ client side
     def submit(self, prompt: list[int]) -> Future:
@@ -188,7 +204,8 @@ class ContinuousBatcher:
         retiring = None  # (requests, collect handle) of sequences found finished
         while True:
             with self._cv:
-                while not self._stop and not self._queue and not self._active and prev is None and retiring is None:
+                while not self._stop and not self._queue and not self._active and prev is None and retiring is None \
+                        and not (self._side_pending is not None and self._side_pending()):
                     self._cv.wait()
                 if self._stop:
                     waiters = list(self._queue) + list(self._active.values()) + \
@@ -245,6 +262,8 @@ class ContinuousBatcher:
                 self.steps += steps
                 TRACER.complete("tutor.decode_chunk", td, cat="tutor", bucket=B, live=len(self._active),
                                 steps=steps)
+            if self._side_work is not None:  # behind the chunk just enqueued, before the next one
+                self._side_work(cur is None and prev is None)
             if retiring is not None:  # gathered behind the chunk before `cur`: ready or nearly
                 self._retire(*retiring)
                 retiring = None

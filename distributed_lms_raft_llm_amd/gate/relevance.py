@@ -58,6 +58,13 @@ class RelevanceGate:
         # the tutoring decode on a shared GPU, at that much more gate latency
         self.max_wait_s = float(os.environ.get("DLMS_GATE_MAX_WAIT_MS", "8")) / 1e3
         self._last_end = 0.0
+        # fill_under_load: under load a pass waits for max_batch queries (up to max_wait_s) instead
+        # of for as long as the previous pass took -- the gate service (gate/service.py) runs the
+        # cross-node batch this way so its passes take as little of the tutor's GPU as possible
+        self.fill_under_load = False
+        # under load, passes run on this stream (a CU-masked one: gate/service.py --cus) so that
+        # they never hold the CUs a co-located tutor's decode kernels are waiting for
+        self.load_stream = None
 
     @classmethod
     def create(cls, model: str = "bert-base-uncased", device: str = "auto", threshold: float = 0.6,
@@ -147,14 +154,21 @@ class RelevanceGate:
                 # slowed the co-located tutor's decode ~2x)
                 now = time.monotonic()
                 busy = now - self._last_end < 0.05
-                wait = min(max(self.window_s, self._last_pass_s if busy else 0.0), self.max_wait_s)
+                if busy and self.fill_under_load:
+                    wait = self.max_wait_s
+                else:
+                    wait = min(max(self.window_s, self._last_pass_s if busy else 0.0), self.max_wait_s)
                 end = now + wait
                 while len(self._pending) < self.max_batch and time.monotonic() < end:
                     self._pcv.wait(max(0.0, end - time.monotonic()))
                 batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
             t_pass = time.monotonic()
             try:
-                with self._lock, torch.no_grad():
+                import contextlib
+
+                ctx = torch.cuda.stream(self.load_stream) if (busy and self.load_stream is not None) else \
+                    contextlib.nullcontext()
+                with self._lock, torch.no_grad(), ctx:
                     q = self.encoder.embed([ids for ids, _, _ in batch]).float()
                     a = torch.stack([x.to(q.device, torch.float32) for _, x, _ in batch])
                     sims = self._cosines(q, a)  # one device->host copy for the whole batch

@@ -195,7 +195,14 @@ def build_arg_parser() -> argparse.ArgumentParser:
     ap.add_argument("--data-dir", default=None, help="default: ./lms_node<id>")
     ap.add_argument("--tutor", default=os.environ.get("DLMS_TUTOR_ADDR", "localhost:50054"),
                     help="tutoring server address ('' to disable)")
-    ap.add_argument("--gate", choices=["bert", "off"], default=os.environ.get("DLMS_GATE", "bert"))
+    ap.add_argument("--gate", choices=["bert", "remote", "off"], default=os.environ.get("DLMS_GATE", "bert"),
+                    help="bert: a BERT encoder in this process (GPU if visible, else CPU torch); remote: the GPU "
+                         "tier's gate servers (--gate-addr), the local encoder only as --gate-fallback")
+    ap.add_argument("--gate-addr", default=os.environ.get("DLMS_GATE_ADDR", ""),
+                    help="gate server addresses, comma-separated (python -m distributed_lms_raft_llm_amd.gate, "
+                         "or tutoring_server.py --gate-port)")
+    ap.add_argument("--gate-fallback", choices=["bert", "off"], default="bert",
+                    help="with --gate remote: what decides when no gate server answers (off: admit)")
     ap.add_argument("--gate-model", default="bert-base-uncased")
     ap.add_argument("--gate-device", default=os.environ.get("DLMS_GATE_DEVICE", "auto"))
     ap.add_argument("--gate-threshold", type=float, default=0.6)
@@ -226,6 +233,20 @@ def main(argv=None):
 
         gate = RelevanceGate.create(model=args.gate_model, device=args.gate_device, threshold=args.gate_threshold,
                                     weights=args.gate_weights, vocab=args.vocab)
+    elif args.gate == "remote":
+        from ..gate.relevance import RelevanceGate
+        from ..gate.service import RemoteGate
+
+        addrs = [a.strip() for a in args.gate_addr.split(",") if a.strip()]
+        if not addrs:
+            raise SystemExit("--gate remote needs --gate-addr")
+        fallback = None
+        if args.gate_fallback == "bert":
+            def fallback():
+                return RelevanceGate.create(model=args.gate_model, device=args.gate_device,
+                                            threshold=args.gate_threshold, weights=args.gate_weights,
+                                            vocab=args.vocab)
+        gate = RemoteGate(addrs, threshold=args.gate_threshold, fallback_factory=fallback)
     srv = LMSServer(args.id, args.port, peers, args.data_dir or f"lms_node{args.id}", host=args.host,
                     advertise=args.advertise, tutor_address=args.tutor or None, gate=gate, raft_config=cfg,
                     fsync=not args.no_fsync, snapshot_every=args.snapshot_every, workers=args.workers,

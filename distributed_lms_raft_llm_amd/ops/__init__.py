@@ -184,6 +184,10 @@ def _bind(L):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    L.dlms_stream_create_cumask.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.dlms_stream_create_cumask.restype = ctypes.c_int
+    L.dlms_stream_destroy.argtypes = [ctypes.c_void_p]
+    L.dlms_stream_destroy.restype = ctypes.c_int
     L.dlms_xgmi_header_bytes.restype = ctypes.c_longlong
     for name in ("dlms_ipc_handle_size", "dlms_xgmi_args_size", "dlms_xgmi_max_blocks"):
         getattr(L, name).restype = ctypes.c_int
@@ -845,6 +849,15 @@ def skinny_gemm(a: torch.Tensor, w_sh: torch.Tensor, epi: int, *, ln=None, bias=
     _check(lib().dlms_skinny_gemm(cepi, _p(a), a.stride(0), _p(lg), _p(lb), le, _p(w_sh), M, N, K, ctypes.byref(ep),
                                   _stream()), "dlms_skinny_gemm")
     return out
+
+
+def cu_masked_stream(n_cus: int) -> "torch.cuda.ExternalStream":
+    """A stream of the current device restricted to ``n_cus`` evenly spread compute units
+    (``hipExtStreamCreateWithCUMask``, api.hip): co-located work that must not hold the CUs a
+    latency-bound decode needs (the relevance gate beside the tutor)."""
+    p = ctypes.c_void_p()
+    _check(lib().dlms_stream_create_cumask(int(n_cus), ctypes.byref(p)), "dlms_stream_create_cumask")
+    return torch.cuda.ExternalStream(p.value)
 
 
 def mid_max_rows(K: int) -> int:

@@ -51,12 +51,17 @@ DEBUG_SERVICE = "lmsinternal.Debug"
 
 # ----------------------------------------------------------------------------- front-end process
 def _frontend_main(path: str, authkey: bytes, idx: int, host: str, vocab, merges, eos: int, timeout: float,
-                   log_level: int):
+                   log_level: int, gate: dict | None = None):
     logging.basicConfig(level=log_level, format=f"%(asctime)s fe{idx} %(name)s %(levelname)s %(message)s")
     from ..tokenizer import GPT2BPE
     from .server import build_prompt
 
     tok = GPT2BPE(vocab, merges, eos_token_id=eos)
+    btok = None
+    if gate is not None:  # the relevance gate served here too: BERT WordPiece on this side of the relay
+        from ..tokenizer import BertWordPiece
+
+        btok = BertWordPiece(gate.get("vocab"), vocab_size=gate["vocab_size"], max_length=gate["max_length"])
     conn = Client(path, family="AF_UNIX", authkey=authkey)
     msg = conn.recv()
     if msg[0] != "ready":
@@ -65,6 +70,7 @@ def _frontend_main(path: str, authkey: bytes, idx: int, host: str, vocab, merges
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
     pending: dict[int, asyncio.Future] = {}
+    gpending: dict[int, asyncio.Future] = {}  # relevance-gate requests (rid -> future of per-item results)
     calls: dict[int, threading.Event] = {}
     replies: dict[int, object] = {}
     outbox: list = []
@@ -94,12 +100,22 @@ def _frontend_main(path: str, authkey: bytes, idx: int, host: str, vocab, merges
             if not f.done():
                 f.set_result((None, "UNAVAILABLE", why))
         pending.clear()
+        for f in gpending.values():
+            if not f.done():
+                f.set_result(None)
+        gpending.clear()
 
     def deliver(items):
         for rid, ids, code, msg_ in items:
             f = pending.pop(rid, None)
             if f is not None and not f.done():
                 f.set_result((ids, code, msg_))
+
+    def gdeliver(items):
+        for rid, res in items:
+            f = gpending.pop(rid, None)
+            if f is not None and not f.done():
+                f.set_result(res)
 
     def reader():  # engine -> front end (own thread: recv blocks)
         while True:
@@ -112,6 +128,8 @@ def _frontend_main(path: str, authkey: bytes, idx: int, host: str, vocab, merges
             kind = m[0]
             if kind == "r":
                 loop.call_soon_threadsafe(deliver, m[1])
+            elif kind == "gr":
+                loop.call_soon_threadsafe(gdeliver, m[1])
             elif kind in ("metrics", "health"):
                 replies[m[1]] = m[2]
                 ev = calls.pop(m[1], None)
@@ -145,6 +163,51 @@ def _frontend_main(path: str, authkey: bytes, idx: int, host: str, vocab, merges
             METRICS.observe("frontend_request_ms", (time.perf_counter() - t0) * 1e3)
             return pb.QueryResponse(success=True, response=tok.decode(out, skip_special_tokens=True))
 
+    async def gate_call(items):
+        """items [(query_ids | None, key, assignment_ids | None)] -> per-item results from the
+        engine's GateWorker (None: the engine is gone)."""
+        if state["dead"] is not None:
+            return None
+        rid = next(rids)
+        fut = loop.create_future()
+        gpending[rid] = fut
+        try:
+            send(("g", [(rid, items)]))
+        except OSError as e:
+            die(f"engine connection lost: {e}")
+        try:
+            return await asyncio.wait_for(fut, timeout)
+        except asyncio.TimeoutError:
+            gpending.pop(rid, None)
+            return None
+
+    def gate_handler(kind):
+        async def h(body: bytes, context) -> bytes:
+            req = json.loads(body) if body else {}
+            if kind == "ScoreBatch":
+                items = [(btok.encode(it["query"]), it["key"],
+                          btok.encode(it["text"]) if it.get("text") is not None else None) for it in req["items"]]
+            elif kind == "Score":
+                items = [(btok.encode(req["query"]), req["key"],
+                          btok.encode(req["text"]) if req.get("text") is not None else None)]
+            else:  # Embed
+                from ..gate.relevance import RelevanceGate
+
+                items = [(None, RelevanceGate._key(req["text"]), btok.encode(req["text"]))]
+            res = await gate_call(items)
+            if res is None:
+                await context.abort(grpc.StatusCode.UNAVAILABLE, state["dead"] or "gate timed out")
+            if kind == "ScoreBatch":
+                out = {"sims": [r if isinstance(r, float) else None for r in res],
+                       "missing": [i for i, r in enumerate(res) if r == "missing"]}
+            elif kind == "Score":
+                out = {"missing": True} if res[0] == "missing" else {"similarity": res[0]}
+            else:
+                out = {"key": items[0][1]}
+            return json.dumps(out).encode()
+
+        return grpc.unary_unary_rpc_method_handler(h)
+
     def ask_engine(kind: str, wait_s: float = 10.0):
         cid = next(rids)
         ev = threading.Event()
@@ -175,6 +238,11 @@ def _frontend_main(path: str, authkey: bytes, idx: int, host: str, vocab, merges
         wire.register(srv, "Tutoring", Servicer())
         srv.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(
             DEBUG_SERVICE, {"Health": debug("health"), "Metrics": debug("metrics")}),))
+        if btok is not None:
+            from ..gate.service import SERVICE as GATE_SERVICE
+
+            srv.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(
+                GATE_SERVICE, {k: gate_handler(k) for k in ("Score", "ScoreBatch", "Embed")}),))
         bound = srv.add_insecure_port(f"{host}:{port}")
         await srv.start()
         send(("bound", bound))
@@ -198,7 +266,10 @@ class FrontendPool:
     the GPU, then ``serve(batcher, health)`` once the engine is up."""
 
     def __init__(self, n: int, port: int, host: str = "[::]", vocab=None, merges=None, eos: int = 50256,
-                 timeout: float = 300.0):
+                 timeout: float = 300.0, gate: dict | None = None):
+        """``gate``: also serve the relevance gate (``lmsinternal.Gate``) on this port -- tokenized in
+        the front ends, scored by ``gate_worker`` (set before ``serve``) between decode chunks;
+        a dict with the BERT tokenizer's ``vocab`` (path or None), ``vocab_size``, ``max_length``."""
         if n < 1:
             raise ValueError("need at least one front end")
         self.n, self.req_port, self.host = n, port, host
@@ -209,7 +280,7 @@ class FrontendPool:
         ctx = mp.get_context("spawn")
         self.procs = [ctx.Process(target=_frontend_main, name=f"tutor-fe{i}", daemon=True,
                                   args=(self.path, self.authkey, i, host, vocab, merges, eos, timeout,
-                                        logging.getLogger().level))
+                                        logging.getLogger().level, gate))
                       for i in range(n)]
         for p in self.procs:
             p.start()
@@ -219,6 +290,8 @@ class FrontendPool:
         self._cv = threading.Condition()
         self._stopping = False
         self.batcher = None
+        self.gate_worker = None
+        self._gout: list[list] = []
 
     def serve(self, batcher, health=None, accept_timeout: float = 120.0):
         """Accept the front ends, hand them the port (the first binds it -- an ephemeral one if
@@ -236,6 +309,7 @@ class FrontendPool:
             self.conns.append(c)
         self.port = port
         self._out = [[] for _ in self.conns]
+        self._gout = [[] for _ in self.conns]
         for i, c in enumerate(self.conns):
             threading.Thread(target=self._reader, args=(i, c), name=f"fe{i}-relay", daemon=True).start()
         threading.Thread(target=self._sender, name="fe-sender", daemon=True).start()
@@ -255,6 +329,11 @@ class FrontendPool:
             self._out[i].append(item)
             self._cv.notify()
 
+    def _gresult(self, i: int, rid: int, res):
+        with self._cv:
+            self._gout[i].append((rid, res))
+            self._cv.notify()
+
     def _reader(self, i: int, c):
         while True:
             try:
@@ -270,6 +349,12 @@ class FrontendPool:
                         f = futures.Future()
                         f.set_exception(e)
                     f.add_done_callback(lambda fut, rid=rid: self._result(i, rid, fut))
+            elif kind == "g":
+                for rid, items in m[1]:
+                    if self.gate_worker is None:
+                        self._gresult(i, rid, None)
+                    else:
+                        self.gate_worker.submit(items, lambda res, rid=rid: self._gresult(i, rid, res))
             elif kind == "metrics":
                 self._send(i, ("metrics", m[1], METRICS.snapshot()))
             elif kind == "health":
@@ -289,17 +374,20 @@ class FrontendPool:
     def _sender(self):
         while True:
             with self._cv:
-                while not self._stopping and not any(self._out):
+                while not self._stopping and not any(self._out) and not any(self._gout):
                     self._cv.wait()
                 if self._stopping:
                     return
                 batches = [(i, o) for i, o in enumerate(self._out) if o]
+                gbatches = [(i, o) for i, o in enumerate(self._gout) if o]
                 self._out = [[] for _ in self.conns]
-                for i, items in batches:
-                    try:
-                        self.conns[i].send(("r", items))
-                    except OSError:
-                        pass
+                self._gout = [[] for _ in self.conns]
+                for kind, bb in (("r", batches), ("gr", gbatches)):
+                    for i, items in bb:
+                        try:
+                            self.conns[i].send((kind, items))
+                        except OSError:
+                            pass
 
     def stop(self, timeout: float = 10.0):
         with self._cv:

@@ -170,6 +170,31 @@ def make_engine(model: str, device: str, max_batch: int, max_length: int, weight
     return TorchGPT2Engine(cfg, w, max_length=max_length)
 
 
+def make_gate_worker(model: str, weights: str | None, device):
+    """The relevance gate's encoder for ``--serve-gate`` (gate/service.py GateWorker): the HIP BERT
+    on the tutor's GPU (its graphs captured now), or the torch reference on a CPU engine."""
+    import torch
+
+    from ..gate.service import GateWorker
+    from ..models.bert import BertReference, init_bert_weights, load_bert_safetensors
+    from ..models.config import bert_config
+
+    cfg = bert_config(model)
+    w = load_bert_safetensors(weights) if weights else init_bert_weights(cfg, seed=0)
+    if str(device).startswith("cuda") and torch.cuda.is_available():
+        from ..engine.bert_engine import HipBertEncoder
+
+        enc = HipBertEncoder(cfg, w, device=device, graph_max_rows=8192, graph_max_seqs=256)
+        enc.warm_graphs()
+    else:
+        enc = BertReference(cfg, w, device="cpu")
+    log.info("relevance gate served on the tutoring port (%s on %s, passes between decode chunks)", model, device)
+    # under load at most one pass per DLMS_GATE_MIN_GAP_MS (fuller passes, fewer stops of the decode
+    # stream); idle, a query is scored at the next batcher iteration
+    return GateWorker(enc, max_seqs=255 if str(device).startswith("cuda") else 127,
+                      min_gap_s=float(os.environ.get("DLMS_GATE_MIN_GAP_MS", "10")) / 1e3)
+
+
 class TutoringServer:
     def __init__(self, engine, port: int = 50054, host: str = "[::]", max_batch: int = 64, window_ms: float = 2.0,
                  max_length: int = 150, repetition_penalty: float = 1.2, tokenizer: GPT2BPE | None = None,
@@ -213,6 +238,10 @@ class TutoringServer:
             out.update(active=b.active, completed=b.completed, ok=b._error is None and b._thread.is_alive())
         else:
             out.update(queued=b.q.qsize(), ok=b._t.is_alive())
+        gw = getattr(getattr(self, "pool", None), "gate_worker", None)
+        if gw is not None:  # --serve-gate: the relevance gate's passes between decode chunks
+            out.update(gate=True, scored=gw.scored, passes=gw.passes, batched_queries=gw.scored,
+                       device=str(getattr(gw.enc, "device", "cpu")))
         return out
 
     def start(self, on_fatal=None, poll_s: float = 0.25):
@@ -401,6 +430,14 @@ def main(argv=None):
     ap.add_argument("--warm-batch", type=int, default=1024,
                     help="capture the decode graphs of every batch bucket up to this size before serving, so "
                          "the first burst of queries does not pay them (0 = capture on first use)")
+    ap.add_argument("--serve-gate", action="store_true",
+                    help="also serve the relevance gate (lmsinternal.Gate) on the tutoring port: the front ends "
+                         "tokenize, this process runs the BERT encoder passes between decode chunks on the decode "
+                         "stream (gate/service.py GateWorker) -- LMS nodes use it with --gate remote "
+                         "--gate-addr <this address>")
+    ap.add_argument("--gate-model", default="bert-base-uncased")
+    ap.add_argument("--gate-vocab", default=None, help="BERT vocab.txt for the gate (synthetic if absent)")
+    ap.add_argument("--gate-weights", default=None, help="local safetensors for the gate model")
     ap.add_argument("--log-level", default=os.environ.get("DLMS_LOG", "INFO"))
     args, _ = parse_with_config(ap, argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
@@ -413,10 +450,15 @@ def main(argv=None):
         tp = args.tp or world
         rank = int(os.environ.get("RANK", "0"))
         if rank % tp == 0:
+            from ..models.config import bert_config
             from .frontend import FrontendPool
 
+            gate_fe = None
+            if args.serve_gate:
+                bc = bert_config(args.gate_model)
+                gate_fe = dict(vocab=args.gate_vocab, vocab_size=bc.vocab_size, max_length=bc.max_position)
             pool = FrontendPool(args.frontends, args.port + rank // tp, args.host, args.vocab, args.merges,
-                                eos=gpt2_config(args.model).eos_token_id)
+                                eos=gpt2_config(args.model).eos_token_id, gate=gate_fe)
     if world > 1:  # torchrun: TP groups of --tp consecutive ranks, one front end (port + group) each
         import torch.distributed as dist
 
@@ -457,6 +499,9 @@ def main(argv=None):
     if pool is not None and hasattr(eng, "admit"):
         srv = PooledTutoringServer(eng, pool, args.max_length, args.repetition_penalty, chunk=args.chunk,
                                    max_queue=args.max_queue)
+        if args.serve_gate:
+            pool.gate_worker = make_gate_worker(args.gate_model, args.gate_weights, getattr(eng, "device", "cpu"))
+            pool.gate_worker.attach(srv.batcher)
     else:
         if pool is not None:  # not a slot engine (CPU window batching): serve in-process
             pool.stop(timeout=2)

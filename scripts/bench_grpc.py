@@ -221,7 +221,7 @@ def _drain(proc, log):
 
 def start_tutor(args, log):
     env = dict(os.environ, PYTHONUNBUFFERED="1")
-    if args.target == "lms" and args.gate == "bert":
+    if args.target == "lms" and args.gate in ("bert", "remote", "remote-proc"):
         # the LMS nodes' BERT gates share the tutor's GPU: its decode chunks on a high-priority stream
         # (LMS path at 3.5 k q/s p50 863 -> 606 ms; alone on the GPU the same setting cost the
         # Tutoring path 16 % at 5.5 k q/s, so it is a co-location setting, not a default)
@@ -235,10 +235,26 @@ def start_tutor(args, log):
                "127.0.0.1", "--max-length", str(args.max_length), "--chunk", str(args.chunk),
                "--model", args.model, "--max-batch", str(args.max_batch), "--frontend", "aio",
                "--frontends", str(args.frontends)]
+        if args.target == "lms" and args.gate == "remote":  # the gate served by the tutor (--serve-gate)
+            cmd += ["--serve-gate"]
     p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     line = _wait_line(p, "Tutoring Server started on port", args.startup_timeout, log)
     _drain(p, log)
-    return p, f"127.0.0.1:{int(line.rsplit(' ', 1)[1])}"
+    addr = f"127.0.0.1:{int(line.rsplit(' ', 1)[1])}"
+    if args.target == "lms" and args.gate == "remote":
+        args.gate_addr = addr
+    return p, addr
+
+
+def start_gate_proc(args, log):
+    """--gate remote-proc: one gate server process on the GPU (python -m distributed_lms_raft_llm_amd.gate)."""
+    cmd = [sys.executable, "-m", "distributed_lms_raft_llm_amd.gate", "--port", "0", "--host", "127.0.0.1"]
+    p = subprocess.Popen(cmd, cwd=ROOT, env=dict(os.environ, PYTHONUNBUFFERED="1"), stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True)
+    line = _wait_line(p, "Gate Server started on port", args.startup_timeout, log)
+    _drain(p, log)
+    args.gate_addr = f"127.0.0.1:{int(line.rsplit(' ', 1)[1])}"
+    return p
 
 
 def _free_ports(n):
@@ -261,12 +277,17 @@ def start_lms(args, tutor_addr, log, tmp):
     procs = []
     for i in range(1, 4):
         peers = [a for j, a in enumerate(addrs, 1) if j != i]
+        remote = args.gate in ("remote", "remote-proc")
         cmd = [sys.executable, "-m", "distributed_lms_raft_llm_amd.lms.server", str(i), str(ports[i - 1]), *peers,
                "--host", "127.0.0.1", "--advertise", addrs[i - 1], "--data-dir", os.path.join(tmp, f"node{i}"),
-               "--tutor", tutor_addr, "--gate", args.gate, "--gate-threshold", str(args.gate_threshold),
+               "--tutor", tutor_addr, "--gate", "remote" if remote else args.gate,
+               "--gate-threshold", str(args.gate_threshold),
                "--workers", str(args.lms_workers), "--frontend", "aio", "--log-level", "WARNING"]
-        p = subprocess.Popen(cmd, cwd=ROOT, env=dict(os.environ, PYTHONUNBUFFERED="1"), stdout=subprocess.PIPE,
-                             stderr=subprocess.STDOUT, text=True)
+        env = dict(os.environ, PYTHONUNBUFFERED="1")
+        if remote:  # GPU-less LMS nodes: the relevance gate is the GPU tier's service
+            cmd += ["--gate-addr", args.gate_addr, "--gate-fallback", "off"]
+            env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         _drain(p, log)
         procs.append(p)
     return procs, addrs
@@ -337,7 +358,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=8)
     ap.add_argument("--null-slots", type=int, default=4096)
     ap.add_argument("--null-step-ms", type=float, default=1.6)
-    ap.add_argument("--gate", choices=("bert", "off"), default="bert")
+    ap.add_argument("--gate", choices=("bert", "remote", "remote-proc", "off"), default="bert",
+                    help="bert: a gate per LMS node on the GPU; remote: ONE gate served by the tutor (passes "
+                         "between decode chunks), LMS nodes GPU-less; remote-proc: a gate server process")
     ap.add_argument("--gate-threshold", type=float, default=0.0, help="0: random-init BERT admits every query")
     ap.add_argument("--lms-workers", type=int, default=32)
     ap.add_argument("--students", type=int, default=64)
@@ -371,6 +394,8 @@ def main():
         t_boot = time.time()
         tutor, tutor_addr = start_tutor(args, log)
         procs.append(tutor)
+        if args.target == "lms" and args.gate == "remote-proc":
+            procs.append(start_gate_proc(args, log))
         if args.target == "lms":
             lms_procs, addrs = start_lms(args, tutor_addr, log, tmp)
             procs += lms_procs
@@ -444,6 +469,12 @@ def main():
                 "dataflow_aborts": c1.get("engine_dataflow_aborts", 0.0) - c0.get("engine_dataflow_aborts", 0.0),
                 "dataflow_aborts_total": c1.get("engine_dataflow_aborts", 0.0),
             }
+            if args.target == "lms" and args.gate in ("remote", "remote-proc"):
+                from distributed_lms_raft_llm_amd.utils.debug_rpc import debug_call
+
+                g = debug_call(args.gate_addr, "Health", timeout=10)
+                line["gate_service"] = {k: g.get(k) for k in ("scored", "missing", "passes", "batched_queries",
+                                                               "device")}
             if lms_m:
                 line["lms_nodes"] = {
                     a: {k: {q: round(v, 2) for q, v in m.get("histograms", {})[k].items() if q in ("count", "p50", "p99")}
