@@ -395,7 +395,9 @@ class HipGPT2Engine:
             if p2p:
                 from ..parallel.xgmi import XgmiComm
 
-                slab = max(self.max_batch * cfg.n_embd * 4, 1 << 20)  # decode messages; big prefills: RCCL
+                # decode messages; big prefills: RCCL (DLMS_XGMI_SLAB_MB: a larger slab keeps packed
+                # prefills on the one-shot kernels too -- the shared-GPU tests, whose group is gloo)
+                slab = max(self.max_batch * cfg.n_embd * 4, int(float(os.environ.get("DLMS_XGMI_SLAB_MB", "1")) * (1 << 20)))
                 self.xgmi = XgmiComm(tp_group, self.device, slab)
 
     # ------------------------------------------------------------------ state
