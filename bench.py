@@ -46,6 +46,11 @@ def metric_for(model: str) -> str:
     return METRIC.replace("GPT-2-124M", MODEL_LABELS.get(model, model))
 
 
+def data_for(model: str) -> str:
+    """The ``data`` field: synthetic prompts and random-init weights of the benchmarked model."""
+    return f"synthetic prompts (random token ids), random-init {MODEL_LABELS.get(model, model)} weights"
+
+
 def vs_baseline(model: str, weight_dtype: str, tok_s: float):
     return round(tok_s / BASELINE_TOK_S, 1) if model == "gpt2" and weight_dtype == "bf16" else None
 
@@ -234,7 +239,7 @@ def main():
             "scaling": "weak" if tp == 1 else "strong",
             "vs_baseline": vs_baseline(args.model, args.weight_dtype, tok_s),
             "dtype": "bf16" if args.weight_dtype == "bf16" else "fp8-w8a8+bf16",
-            "data": "synthetic prompts (random token ids), random-init GPT-2-124M weights",
+            "data": data_for(args.model),
             "p50_query_latency_ms": round(p50, 3),
             "baseline_p50_query_latency_ms": 2198,
             "new_tokens_per_step": total_new / args.steps,

@@ -101,3 +101,5 @@ def test_bench_labels_are_model_correct():
     assert bench.vs_baseline("gpt2", "bf16", 53.7 * 10) == 10.0
     assert bench.vs_baseline("gpt2-medium", "bf16", 1e5) is None
     assert bench.vs_baseline("gpt2", "fp8", 1e5) is None
+    assert "GPT-2-XL" in bench.data_for("gpt2-xl") and "124M" not in bench.data_for("gpt2-xl")
+    assert "GPT-2-124M" in bench.data_for("gpt2")

@@ -252,8 +252,9 @@ def test_production_throughput_path_matches_fp32_oracle():
     """The exact path every BENCH step runs -- default knobs, the BENCH shape: 1024 rows of
     32-token prompts to max_length 150, i.e. two 512-row parts on HIP streams (overlap_min_batch
     512), split-K cap 2, 768-block persistent attention, 8 decode steps per graph replay, the
-    panel-resident LM head, the LayerNorms folded into the GEMMs (round 5), and the 64x96 GEMM tiles
-    of 256 < M <= 512 (QKV + K/V scatter, c_fc + GELU, c_proj split 4 reduced in-kernel) -- with the
+    panel-resident LM head, LN1 fused into ``decode_update`` and the split-K slabs summed by
+    ``add_layernorm``, and the 64x96 GEMM tiles of 256 < M <= 512 (QKV + K/V scatter, c_fc + GELU,
+    c_proj) -- with the
     64x96 dispatch asserted from the launch census and every row checked against the fp32 oracle
     with the margin rule (VERDICT r3 next #4)."""
     from distributed_lms_raft_llm_amd import ops
