@@ -39,6 +39,22 @@ from .weights import GPT2DeviceWeights, prepare_gpt2_weights
 
 log = logging.getLogger(__name__)
 
+# Streams of this process that run work beside the engine's decode (a co-located gate's encoder, a
+# test's load generator).  An aborted dataflow launch records whether one of them was busy: the
+# dataflow grid's workgroups wait on each other, so a kernel on another stream that holds CUs can
+# leave part of the grid unscheduled until the bounded waits give up.
+_SIDE_STREAMS: list = []
+
+
+def register_side_stream(stream) -> None:
+    """Declare a stream whose kernels may run beside the engine's decode (see ``_SIDE_STREAMS``)."""
+    if all(s is not stream for s in _SIDE_STREAMS):
+        _SIDE_STREAMS.append(stream)
+
+
+def unregister_side_stream(stream) -> None:
+    _SIDE_STREAMS[:] = [s for s in _SIDE_STREAMS if s is not stream]
+
 
 @dataclass
 class GenerateStats:
@@ -382,6 +398,7 @@ class HipGPT2Engine:
         self._df_status = None  # the last decode() launch's error words in flight (dataflow_status_async)
         self._df_off_until = 0.0  # after an aborted launch: launch-per-op until then (DLMS_DF_COOLDOWN_S)
         self.df_aborts = 0
+        self.df_aborts_beside_side_work = 0  # of those, aborts while a registered side stream was busy
         self._side_streams: list[torch.cuda.Stream] = []
         self._flags: torch.Tensor | None = None
         self._graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
@@ -764,8 +781,13 @@ class HipGPT2Engine:
 
         self.df_aborts += 1
         METRICS.inc("engine_dataflow_aborts")
+        beside = any(not st_.query() for st_ in _SIDE_STREAMS)
+        if beside:
+            self.df_aborts_beside_side_work += 1
+            METRICS.inc("engine_dataflow_aborts_beside_side_work")
         self._df_off_until = time.monotonic() + float(os.environ.get("DLMS_DF_COOLDOWN_S", "30"))
-        log.warning("%s (committed %d steps); launch-per-op for a while", DataflowDecoder.describe(st), st[4])
+        log.warning("%s (committed %d steps%s); launch-per-op for a while", DataflowDecoder.describe(st), st[4],
+                    ", a side stream busy" if beside else "")
 
     def dataflow_status_async(self) -> "HostResult | None":
         """Whether the last ``decode()`` chunk ran the dataflow kernel and it ABORTED before

@@ -229,6 +229,43 @@ def test_dataflow_injected_abort_generate_falls_back():
     assert decisive >= 0.7 * total
 
 
+def test_dataflow_beside_a_long_kernel_on_another_stream():
+    """the dataflow grid's workgroups wait on each other, and nothing reserves the CUs
+    against a kernel that another stream of the same process has in flight.  With 8192^3 GEMMs
+    streaming on a second stream through the whole decode, the launch either completes or aborts
+    cleanly (bounded waits, nothing committed) and the rows are decoded launch-per-op: the tokens
+    hold the fp32 oracle either way, and every abort is counted as one beside side work."""
+    from distributed_lms_raft_llm_amd.engine import gpt2_engine as ge
+
+    cfg, w = _setup("gpt2")
+    prompts = _prompts(cfg, [32], seed=5)
+    eng = _engine(cfg, w, True, max_batch=2, max_length=150)
+    ref = eng.generate(prompts)  # warm (graphs, dataflow plan) and the unloaded answer
+    assert eng.df_aborts == 0
+    side = torch.cuda.Stream()
+    a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    c = torch.empty_like(a)
+    ge.register_side_stream(side)
+    try:
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(80):  # ~0.7 ms each: busy through the ~27 ms decode
+                torch.mm(a, a, out=c)
+        out = eng.generate(prompts)
+        overlapped = not side.query()
+        side.synchronize()
+    finally:
+        ge.unregister_side_stream(side)
+    print(f"side stream still busy after the decode: {overlapped}; aborts {eng.df_aborts} "
+          f"(beside side work {eng.df_aborts_beside_side_work})")
+    assert eng.df_aborts_beside_side_work == eng.df_aborts
+    total, decisive = _oracle(cfg, w, out, prompts)
+    assert total == 150 - 32 or out[0][-1] == cfg.eos_token_id
+    assert decisive >= 0.7 * total
+    if eng.df_aborts == 0:
+        assert out == ref  # completed on the dataflow path: the same tokens as unloaded
+
+
 def test_batcher_single_slot_runs_dataflow_and_matches_oracle():
     """The tutor's low-load operating point: one live request at a time through the
     ContinuousBatcher -> slot 0 -> bucket 1 -> the dataflow kernel in chunks of 8 steps; every

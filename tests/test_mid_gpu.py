@@ -147,10 +147,11 @@ def _engine_setup(name="gpt2", seed=0):
     return cfg, w
 
 
-@pytest.mark.parametrize("name,batch", [("gpt2", 9), ("gpt2", 16), ("gpt2", 32), ("gpt2-medium", 24)])
+@pytest.mark.parametrize("name,batch", [("gpt2", 3), ("gpt2", 8), ("gpt2", 9), ("gpt2", 16), ("gpt2", 32),
+                                        ("gpt2", 64), ("gpt2-medium", 24)])
 def test_mid_path_generate_matches_fp32_oracle(name, batch):
     """The mid-batch decode step (mid.hip LN-fused GEMMs + in-place projections) is the path taken at
-    9-32 rows, its tokens match the fp32 oracle under the margin rule, and graph replay equals
+    3-64 rows, its tokens match the fp32 oracle under the margin rule, and graph replay equals
     eager launch bit for bit."""
     from distributed_lms_raft_llm_amd.engine.gpt2_engine import HipGPT2Engine
     from distributed_lms_raft_llm_amd.models.gpt2 import GPT2Reference, teacher_forced_check
