@@ -221,7 +221,7 @@ class HipBertEncoder:
             self._run_layers(*args)
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        with torch.cuda.graph(graph):
             self._run_layers(*args)
         return graph
 

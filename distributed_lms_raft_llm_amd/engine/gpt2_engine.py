@@ -1016,7 +1016,10 @@ class HipGPT2Engine:
             # (one graph per row part replayed on its own stream measured identical to this one
             # forked graph: 668.07 vs 668.08 k tok/s, profiles/r2_sweep_split_graphs.jsonl)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            # default (global) capture mode: no other thread issues GPU work while the engine
+            # captures (the served gate runs on the batcher thread), and the round-6 GPU tier saw a
+            # host segfault in hipGraphLaunch replaying a graph captured in thread_local mode
+            with torch.cuda.graph(g):
                 self._decode_step(B, penalty, nsteps)
             self._restore_state(B, saved)
             self._graphs[key] = g
@@ -1183,7 +1186,7 @@ class HipGPT2Engine:
             args = (d[:R], d[R:2 * R], d[2 * R:3 * R], d[o:o + n], d[o + n:o + 2 * n], d[o + 2 * n:o + 3 * n], tiles,
                     penalty)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g):
                 self._prefill_core(*args)
             st["graph"], st["penalty"] = g, penalty
         st["graph"].replay()
