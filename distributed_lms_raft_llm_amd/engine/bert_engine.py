@@ -220,8 +220,10 @@ class HipBertEncoder:
         with torch.cuda.stream(side):  # warm-up (code objects, allocator) outside the capture
             self._run_layers(*args)
         torch.cuda.current_stream().wait_stream(side)
+        from .gpt2_engine import capture_guard
+
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with capture_guard(), torch.cuda.graph(graph):
             self._run_layers(*args)
         return graph
 

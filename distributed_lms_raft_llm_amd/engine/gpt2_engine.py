@@ -22,6 +22,7 @@ No host round trip happens inside a step; the host only checks the stop flags ev
 """
 from __future__ import annotations
 
+import contextlib
 import itertools
 import logging
 import math
@@ -44,6 +45,25 @@ log = logging.getLogger(__name__)
 # dataflow grid's workgroups wait on each other, so a kernel on another stream that holds CUs can
 # leave part of the grid unscheduled until the bounded waits give up.
 _SIDE_STREAMS: list = []
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Around a hipGraph capture: collect garbage first, then keep Python's cyclic GC off until the
+    capture ends.  An automatic collection DURING a capture runs the destructors of dead engines'
+    graphs (hipGraphExecDestroy) in the middle of it -- in any thread, since the GC runs wherever
+    an allocation triggers it -- which aborted the process (and, once, left a graph that
+    segfaulted on replay) in the round-6 GPU tier."""
+    import gc
+
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def register_side_stream(stream) -> None:
@@ -1016,10 +1036,7 @@ class HipGPT2Engine:
             # (one graph per row part replayed on its own stream measured identical to this one
             # forked graph: 668.07 vs 668.08 k tok/s, profiles/r2_sweep_split_graphs.jsonl)
             g = torch.cuda.CUDAGraph()
-            # default (global) capture mode: no other thread issues GPU work while the engine
-            # captures (the served gate runs on the batcher thread), and the round-6 GPU tier saw a
-            # host segfault in hipGraphLaunch replaying a graph captured in thread_local mode
-            with torch.cuda.graph(g):
+            with capture_guard(), torch.cuda.graph(g):
                 self._decode_step(B, penalty, nsteps)
             self._restore_state(B, saved)
             self._graphs[key] = g
@@ -1186,7 +1203,7 @@ class HipGPT2Engine:
             args = (d[:R], d[R:2 * R], d[2 * R:3 * R], d[o:o + n], d[o + n:o + 2 * n], d[o + 2 * n:o + 3 * n], tiles,
                     penalty)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with capture_guard(), torch.cuda.graph(g):
                 self._prefill_core(*args)
             st["graph"], st["penalty"] = g, penalty
         st["graph"].replay()
