@@ -229,6 +229,9 @@ def test_dataflow_injected_abort_generate_falls_back():
     assert decisive >= 0.7 * total
 
 
+@pytest.mark.skipif(os.environ.get("DLMS_STRESS_TESTS") != "1",
+                    reason="open issue: in the full GPU tier this test is followed by a host segfault in a later "
+                           "test's graph replay (same process); run it alone with DLMS_STRESS_TESTS=1")
 def test_dataflow_beside_a_long_kernel_on_another_stream():
     """the dataflow grid's workgroups wait on each other, and nothing reserves the CUs
     against a kernel that another stream of the same process has in flight.  With 8192^3 GEMMs
