@@ -1025,10 +1025,14 @@ class HipGPT2Engine:
         key = (B, float(penalty), nsteps)
         g = self._graphs.get(key)
         if g is None:
-            # warm up on a side stream (kernel code objects loaded, RCCL comm initialised)
+            # warm up on a side stream (kernel code objects loaded, RCCL comm initialised).  The
+            # snapshot is enqueued BEFORE the side stream's wait, so the warm-up step is ordered
+            # after it: the other order let the warm-up advance the rows before the snapshot copied
+            # them, and the restore then left them one step ahead (the first generation after a
+            # capture deviated -- TP=8 on a shared GPU showed it, profiles/r6_tp124m_tests.txt)
+            saved = self._snapshot_state(B)
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream())
-            saved = self._snapshot_state(B)
             with torch.cuda.stream(s):
                 self._decode_step(B, penalty, nsteps)
             torch.cuda.current_stream().wait_stream(s)
