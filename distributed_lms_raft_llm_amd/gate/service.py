@@ -407,11 +407,9 @@ class GateWorker:
         if self.batcher is not None:
             self.batcher.kick()
 
-    def _split(self, items, cb):
-        """(head, tail) requests of one oversized request: head fits one pass (half the sequence
-        budget each for queries and their new assignments), tail is the rest; cb gets the results
-        of both, in item order, once both have them."""
-        n = max(1, self.max_seqs // 2)
+    def _split(self, items, cb, n: int):
+        """(head, tail) of one request that does not fit the pass being packed: head = its first n
+        items, tail = the rest; cb gets the results of both, in item order, once both have them."""
         got = [None, None]
 
         def part(idx):
@@ -423,6 +421,20 @@ class GateWorker:
 
         return (items[:n], part(0)), (items[n:], part(1))
 
+    def _need(self, items, new_keys, limit: int | None = None):
+        """Encoder sequences the items need (a query each, plus each assignment neither cached nor
+        already in this pass); with ``limit``: how many leading items fit in ``limit`` sequences."""
+        n, seen = 0, set()
+        for i, (q, k, a) in enumerate(items):
+            add = q is not None
+            add += a is not None and k not in seen and k not in new_keys and self._cached(k) is None
+            if limit is not None and n + add > limit:
+                return i
+            n += add
+            if a is not None:
+                seen.add(k)
+        return len(items) if limit is not None else n
+
     def pending(self) -> bool:
         return bool(self._pending) or bool(self._inflight)
 
@@ -433,8 +445,6 @@ class GateWorker:
         return v
 
     def work(self, idle: bool):
-        import torch
-
         while self._inflight:
             ev = self._inflight[0][0]
             if idle:
@@ -442,34 +452,45 @@ class GateWorker:
             if not ev.query():
                 break
             self._deliver()
-        if len(self._inflight) >= self.max_inflight or not self._pending:
-            return
         now = time.monotonic()
         if not idle and now - self._last_start < self.min_gap_s:
             return
-        # one pass: as many requests as fit in max_seqs encoder sequences (a request larger than
-        # that is split across passes: its callback fires once every item has a result)
+        # up to max_inflight passes back to back between two decode chunks (one pass per chunk
+        # capped the served gate at ~2.35 k queries/s at 5.5 k q/s offered: profiles/r6_gate_tier_final.jsonl)
+        while self._pending and len(self._inflight) < self.max_inflight:
+            if not self._one_pass(now):
+                break
+
+    def _one_pass(self, now: float) -> bool:
+        """Pack and enqueue one encoder pass; False when no request could be taken."""
+        import torch
+
+        # one pass: requests packed into max_seqs encoder sequences; the request that does not fit
+        # any more is split so its head fills the pass (its callback fires once every item has a
+        # result) -- whole-request packing left passes half full when requests were large
         with self._lock:
             take, nseq, new_keys = [], 0, {}
-            while self._pending:
+            while self._pending and nseq < self.max_seqs:
                 items, cb = self._pending[0]
-                need = sum(1 for q, _, _ in items if q is not None)
-                need += sum(1 for q, k, a in items if a is not None and self._cached(k) is None and k not in new_keys)
-                if take and nseq + need > self.max_seqs:
-                    break
-                if not take and need > self.max_seqs:  # split: this pass takes the first part
-                    head, tail = self._split(items, cb)
+                need = self._need(items, new_keys)
+                if nseq + need <= self.max_seqs:
+                    self._pending.pop(0)
+                else:
+                    room = self.max_seqs - nseq
+                    cnt = self._need(items, new_keys, limit=room)
+                    if cnt == 0 or (take and room < 16):  # not worth a split for a sliver
+                        break
+                    head, tail = self._split(items, cb, cnt)
                     self._pending[0] = tail
                     items, cb = head
-                    need = sum(1 for q, _, _ in items if q is not None) + \
-                        sum(1 for q, k, a in items if a is not None and self._cached(k) is None)
-                else:
-                    self._pending.pop(0)
+                    need = self._need(items, new_keys)
                 take.append((items, cb))
                 nseq += need
                 for q, k, a in items:
                     if a is not None and self._cached(k) is None:
                         new_keys.setdefault(k, a)
+        if not take:
+            return False
         seqs, qrefs = [], []  # qrefs: (request index, item index, assignment key)
         results = [[None] * len(items) for items, _ in take]
         for ri, (items, _) in enumerate(take):
@@ -486,7 +507,7 @@ class GateWorker:
         self._last_start = now
         if not seqs:
             self._finish(None, take, results, qrefs)
-            return
+            return True
         with torch.no_grad():
             pooled = self.enc.embed(seqs).float()
             for j, k in enumerate(keys):
@@ -514,6 +535,7 @@ class GateWorker:
             self._inflight.append((ev, host, take, results, qrefs))
         else:
             self._finish(host, take, results, qrefs)
+        return True
 
     def _deliver(self):
         _, host, take, results, qrefs = self._inflight.popleft()

@@ -198,3 +198,31 @@ def test_gate_worker_splits_oversized_requests():
     local = _gate()
     assert abs(out[0][5] - local.similarity("query number 5", text)) < 1e-4
     assert w.passes >= 3
+
+
+def test_gate_worker_fills_passes_across_requests():
+    """Passes are packed full: the request that no longer fits is split so its head fills the pass
+    (two 40-query requests, 64 sequences per pass -> 2 passes, not 3), and both callers get every
+    result in item order."""
+    from distributed_lms_raft_llm_amd.gate.service import GateWorker
+    from distributed_lms_raft_llm_amd.models.bert import BertReference, init_bert_weights
+    from distributed_lms_raft_llm_amd.models.config import bert_config
+    from distributed_lms_raft_llm_amd.tokenizer import BertWordPiece
+
+    bc = bert_config("bert-tiny")
+    w = GateWorker(BertReference(bc, init_bert_weights(bc, seed=0)), max_seqs=64)
+    tok = BertWordPiece(None, vocab_size=bc.vocab_size, max_length=bc.max_position)
+    text = "consensus with a replicated log"
+    w.submit([(None, "k", tok.encode(text))], lambda r: None)  # embed the assignment first
+    while w.pending():
+        w.work(True)
+    assert w.passes == 1
+    outs = [[], []]
+    for r in range(2):
+        w.submit([(tok.encode(f"request {r} query {i}"), "k", None) for i in range(40)], outs[r].append)
+    while w.pending():
+        w.work(True)
+    assert w.passes == 1 + 2
+    assert [len(o) for o in outs] == [1, 1] and len(outs[0][0]) == 40 and len(outs[1][0]) == 40
+    local = _gate()
+    assert abs(outs[1][0][33] - local.similarity("request 1 query 33", text)) < 1e-4
