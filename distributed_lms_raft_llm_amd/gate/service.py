@@ -391,7 +391,7 @@ class GateWorker:
         self._lock = threading.Lock()
         self._pending: list = []  # (items, cb)
         self._inflight = __import__("collections").deque()  # passes enqueued, oldest first
-        self.max_inflight = 2
+        self.max_inflight = 4  # passes in flight = passes per decode-chunk gap under load
         self._last_start = 0.0
         self.passes = 0
         self.scored = 0
