@@ -78,7 +78,6 @@ class HipBertEncoder:
     # sequences, sequence slots to a power of two; larger passes run eagerly
     GRAPH_MAX_ROWS = 4096
     GRAPH_MAX_SEQS = 128
-    STAGING_RING = 8  # pinned staging buffers per bucket (passes in flight without a host wait)
 
     @torch.no_grad()
     def embed(self, batch: list[list[int]]) -> torch.Tensor:
@@ -142,14 +141,9 @@ class HipBertEncoder:
         TB = Rb // 16 + min(nb, Rb)  # >= any tile count of Rb rows in <= nb sequences (padding
         # tiles repeat the last one; they run beside the real ones, on otherwise idle CUs)
         words = 4 * Rb + 2 * nb + 2 * TB
-        # a ring of pinned staging buffers: passes enqueued back to back (the served gate runs
-        # several between two decode chunks, each queued behind the chunk) must not wait for the
-        # previous pass's upload to leave its staging buffer -- with one buffer the host blocked
-        # for a whole decode chunk per extra pass and the decode pipeline ran dry
-        ring = self.STAGING_RING
-        st = dict(hosts=[torch.empty(words, dtype=torch.int32).pin_memory() for _ in range(ring)],
-                  events=[torch.cuda.Event() for _ in range(ring)], next=0,
-                  dev=torch.empty(words, dtype=torch.int32, device=dev), TB=TB, graph=None)
+        st = dict(host=torch.empty(words, dtype=torch.int32).pin_memory(),
+                  dev=torch.empty(words, dtype=torch.int32, device=dev), TB=TB, graph=None,
+                  copied=torch.cuda.Event())
         self._gstate[(Rb, nb)] = st
         return st
 
@@ -181,11 +175,8 @@ class HipBertEncoder:
         lens_all = np.concatenate([lens_np, np.asarray(dummy, dtype=np.int64)])
         st = self._graph_state(Rb, nb)
         TB = st["TB"]
-        slot = st["next"]
-        st["next"] = (slot + 1) % len(st["hosts"])
-        st["events"][slot].synchronize()  # this staging buffer's last upload has left it
-        host_t = st["hosts"][slot]
-        host = host_t.numpy()
+        st["copied"].synchronize()  # the previous pass's upload has left the staging buffer
+        host = st["host"].numpy()
         ends = np.cumsum(lens_all)
         starts_np = ends - lens_all
         host[:Rb] = 0  # dummy rows: token 0
@@ -205,8 +196,8 @@ class HipBertEncoder:
         tt[len(tiles):] = tiles[-1]  # padding tiles repeat the last one: identical rows, identical values
         host[o + 2 * nb:] = tt.reshape(-1)
         d = st["dev"]
-        d.copy_(host_t, non_blocking=True)
-        st["events"][slot].record()
+        d.copy_(st["host"], non_blocking=True)
+        st["copied"].record()
         if st["graph"] is None:
             st["graph"] = self._capture(st, Rb, nb)
         st["graph"].replay()
